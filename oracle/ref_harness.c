@@ -1,0 +1,129 @@
+/*
+ * ref_harness.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Drives the REAL reference (compiled from /root/reference by oracle/Makefile into
+ * oracle/_ref/libref.so, never committed) over a packed batch and emits the
+ * canonical records of oracle/rhp_oracle.h.  Used to pin the restatement
+ * (oracle/diff_fuzz.c) and to generate tests/golden/ fixtures.
+ *
+ *   phr_parse_request  src/picohttpparser/picohttpparser.c:383-409
+ *   http_read_request  src/reactor/http.c:177-234 (driven like test/http.c:121-141,
+ *                      but with the stream's input pointing into the batch so the
+ *                      bytes after each request are the batch's own bytes)
+ */
+#include <string.h>
+#include <reactor.h>
+#include "picohttpparser/picohttpparser.h"
+#include "rhp_oracle.h"
+
+static void ref_canon(orc_req_t *r, orc_hdr_t *h, uint32_t max_headers)
+{
+  int32_t ret = r->ret;
+  memset(r, 0, sizeof *r);
+  r->ret = ret;
+  memset(h, 0, sizeof *h * max_headers);
+}
+
+static int ref_phr_one(const uint8_t *buf, size_t len, orc_req_t *req, orc_hdr_t *hdrs,
+                       uint32_t max_headers, struct phr_header *tmp)
+{
+  const char *method, *path;
+  size_t method_len, path_len, num = max_headers;
+  int minor;
+  int r = phr_parse_request((const char *) buf, len, &method, &method_len, &path, &path_len, &minor,
+                            tmp, &num, 0);
+  memset(req, 0, sizeof *req);
+  req->ret = r;
+  if (r > 0) {
+    req->minor_version = minor;
+    req->num_headers = (uint32_t) num;
+    req->method_off = method - (const char *) buf;
+    req->method_len = (int64_t) method_len;
+    req->path_off = path - (const char *) buf;
+    req->path_len = (int64_t) path_len;
+    for (size_t i = 0; i < num; i++) {
+      hdrs[i].name_off = tmp[i].name ? tmp[i].name - (const char *) buf : -1;
+      hdrs[i].name_len = (int64_t) tmp[i].name_len;
+      hdrs[i].value_off = tmp[i].value - (const char *) buf;
+      hdrs[i].value_len = (int64_t) tmp[i].value_len;
+    }
+  }
+  return r;
+}
+
+void ref_phr_batch(const uint8_t *bytes, const uint64_t *offsets, uint32_t n,
+                   uint32_t max_headers, orc_req_t *reqs, orc_hdr_t *hdrs)
+{
+  struct phr_header tmp[256];
+  if (max_headers > 256)
+    max_headers = 256;
+  for (uint32_t i = 0; i < n; i++) {
+    orc_hdr_t *h = hdrs + (size_t) i * max_headers;
+    memset(h, 0, sizeof *h * max_headers);
+    int r = ref_phr_one(bytes + offsets[i], offsets[i + 1] - offsets[i], &reqs[i], h, max_headers, tmp);
+    if (r <= 0)
+      ref_canon(&reqs[i], h, max_headers);
+  }
+}
+
+void ref_http_batch(uint8_t *bytes, const uint64_t *offsets, uint32_t n,
+                    uint32_t max_headers, orc_req_t *reqs, orc_hdr_t *hdrs,
+                    orc_http_t *https)
+{
+  struct phr_header tmp[256];
+  http_field_t fields[256];
+  if (max_headers > 256)
+    max_headers = 256;
+  for (uint32_t i = 0; i < n; i++) {
+    uint8_t *buf = bytes + offsets[i];
+    size_t len = offsets[i + 1] - offsets[i];
+    orc_hdr_t *h = hdrs + (size_t) i * max_headers;
+    memset(h, 0, sizeof *h * max_headers);
+    memset(&https[i], 0, sizeof https[i]);
+
+    /* minor_version is local to http_read_request; take it from phr on the
+     * untouched bytes (http.c:188-192 calls phr with the same arguments) */
+    orc_req_t pre;
+    ref_phr_one(buf, len, &pre, h, max_headers, tmp);
+    memset(h, 0, sizeof *h * max_headers);
+
+    stream_t s;
+    memset(&s, 0, sizeof s);
+    s.fd = -1;
+    s.input.data = data(buf, len);
+    s.input.capacity = len;
+    s.input_consumed = 0;
+    string_t method = string_null(), target = string_null();
+    data_t body = data_null();
+    size_t count = max_headers;
+    int r = http_read_request(&s, &method, &target, &body, fields, &count);
+
+    orc_req_t *req = &reqs[i];
+    memset(req, 0, sizeof *req);
+    https[i].result = r;
+    if (r == 1) {
+      req->ret = pre.ret;
+      req->minor_version = pre.minor_version;
+      req->num_headers = (uint32_t) count;
+      req->method_off = (const uint8_t *) data_base(method) - buf;
+      req->method_len = (int64_t) data_size(method);
+      req->path_off = (const uint8_t *) data_base(target) - buf;
+      req->path_len = (int64_t) data_size(target);
+      for (size_t k = 0; k < count; k++) {
+        h[k].name_off = data_base(fields[k].name) ? (const uint8_t *) data_base(fields[k].name) - buf : -1;
+        h[k].name_len = (int64_t) data_size(fields[k].name);
+        h[k].value_off = (const uint8_t *) data_base(fields[k].value) - buf;
+        h[k].value_len = (int64_t) data_size(fields[k].value);
+      }
+      https[i].consumed = (uint64_t) s.input_consumed;
+      if (data_base(body)) {
+        https[i].body_kind = 1;
+        https[i].body_off = (const uint8_t *) data_base(body) - buf;
+        https[i].body_len = (uint64_t) data_size(body);
+      }
+    } else {
+      req->ret = pre.ret;
+      ref_canon(req, h, max_headers);
+    }
+  }
+}

@@ -1,0 +1,116 @@
+/*
+ * rhp.h -- MI355X batched HTTP/1.1 request parser: the C-ABI drop-in boundary.
+ *
+ * Replaces, for a batch of independent request buffers already in HBM:
+ *   int phr_parse_request(const char *buf, size_t len, const char **method,
+ *       size_t *method_len, const char **path, size_t *path_len, int *minor_version,
+ *       struct phr_header *headers, size_t *num_headers, size_t last_len);
+ *                       /root/reference/src/picohttpparser/picohttpparser.h:51-52
+ *   int http_read_request(stream_t *, string_t *method, string_t *target, data_t *body,
+ *       http_field_t *fields, size_t *fields_count);
+ *                       /root/reference/src/reactor/http.h:36 (http.c:177-234)
+ *
+ * One call parses n requests.  Request i is bytes[offsets[i] .. offsets[i+1]) (its
+ * `len`); the bytes after it (the next request, then >= RHP_PAD zero bytes after
+ * the last one) are what the reference would read past the end.
+ * Every pointer the reference returns into `buf` is returned here as an offset
+ * from the request start (pointer - buf).  All buffers are device memory owned by
+ * the caller; the call is asynchronous on `stream` (a hipStream_t).
+ *
+ * Records are compact (u16 offsets): a request longer than RHP_MAX_LEN bytes gets
+ * ret = RHP_RET_TOOLONG and no other output.
+ */
+#ifndef RHP_H
+#define RHP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RHP_PAD 256u            /* zero bytes required after the last request */
+#define RHP_MAX_LEN 65535u      /* longest request the u16 record format holds */
+#define RHP_MAX_HEADERS 64u     /* largest supported *num_headers capacity */
+#define RHP_RET_TOOLONG (-3)
+
+enum rhp_mode {
+  RHP_MODE_PHR = 0,   /* phr_parse_request(buf, len, ..., &num_headers = max, last_len = 0) */
+  RHP_MODE_HTTP = 1   /* http_read_request over a stream whose unconsumed input is the request */
+};
+
+/* phr_parse_request result for one request (16 B).  For ret <= 0 only `ret`
+ * is meaningful (the reference leaves the other outputs unspecified). */
+typedef struct rhp_req {
+  int32_t  ret;            /* >0 bytes consumed, -1 malformed, -2 partial, RHP_RET_TOOLONG */
+  uint16_t method_len;
+  uint16_t path_off;
+  uint16_t path_len;
+  uint8_t  method_off;     /* 0, 1 or 2 (one optional leading CRLF / LF) */
+  int8_t   minor_version;
+  uint16_t num_headers;
+  uint16_t flags;          /* RHP_F_* diagnostics, not part of parity */
+} rhp_req_t;
+
+#define RHP_F_EXACT 0x1u   /* resolved by the exact (scalar) device path, not the DFA */
+
+/* struct phr_header as offsets (8 B); name_off == RHP_NAME_NULL encodes name ==
+ * NULL (obs-fold continuation line, picohttpparser.c:318-321). */
+typedef struct rhp_hdr {
+  uint16_t name_off, name_len;
+  uint16_t value_off, value_len;
+} rhp_hdr_t;
+
+#define RHP_NAME_NULL 0xFFFFu
+
+/* http_read_request result (24 B), RHP_MODE_HTTP only */
+typedef struct rhp_http {
+  int32_t  result;         /* 1 ready, 0 need more bytes / empty, -1 malformed */
+  uint32_t body_kind;      /* 0: data_null(); 1: body = (req.ret, body_len) */
+  uint64_t consumed;       /* bytes stream_consume() is given (mod 2^64, http.c:216) */
+  uint64_t body_len;
+} rhp_http_t;
+
+typedef struct rhp_batch {
+  const uint8_t  *bytes;   /* device: packed requests + RHP_PAD zero bytes */
+  uint8_t        *bytes_rw;/* device, RHP_MODE_HTTP: same buffer, writable (chunked
+                              bodies are de-framed in place, http.c:134-160); may be NULL
+                              in RHP_MODE_PHR */
+  const uint64_t *offsets; /* device: n + 1 offsets, non-decreasing */
+  uint64_t        bytes_size; /* readable bytes at `bytes` (>= offsets[n] + RHP_PAD) */
+  uint32_t        n;
+  uint32_t        max_headers; /* headers capacity per request (*num_headers in) */
+  uint32_t        mode;        /* enum rhp_mode */
+  uint32_t        reserved;
+  rhp_req_t      *reqs;        /* device [n] */
+  rhp_hdr_t      *hdrs;        /* device [n * max_headers] */
+  rhp_http_t     *http;        /* device [n], RHP_MODE_HTTP */
+  uint32_t       *work;        /* device scratch, >= RHP_WORK_WORDS u32: zero it once before
+                                  the first call; every call leaves it zeroed again.  One
+                                  `work` per concurrently running call. */
+} rhp_batch_t;
+
+#define RHP_WORK_WORDS 64u
+
+/* Parse a batch on `stream` (hipStream_t).  Returns 0 on successful launch,
+ * a negative errno-style code for bad arguments, or a positive hipError_t. */
+int rhp_parse_batch(const rhp_batch_t *batch, void *stream);
+
+/* Which kernel implementation rhp_parse_batch uses (diagnostics / A-B tests). */
+enum rhp_impl {
+  RHP_IMPL_DFA = 0,    /* lane-per-request byte DFA with LDS tables (default) */
+  RHP_IMPL_EXACT = 1   /* lane-per-request exact scalar path only (slow reference path) */
+};
+int rhp_set_impl(int impl);
+
+/* Name of the kernel symbol the default implementation launches (for profiles). */
+const char *rhp_kernel_name(void);
+
+/* Library version string. */
+const char *rhp_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

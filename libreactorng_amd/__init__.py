@@ -1,0 +1,210 @@
+"""libreactorng_amd -- MI355X-native batched HTTP/1.1 request parser (rhp).
+
+Python plumbing over the C-ABI in include/rhp.h (librhp.so, HIP/gfx950) and the
+host helpers in include/rhp_gen.h (librhp_host.so).  The product path is the HIP
+kernel: `parse_batch` raises if librhp.so is missing or no GPU is visible; it
+never falls back to a CPU parser.
+
+Reference interface mirrored (record fields are offsets from each request start):
+  phr_parse_request   /root/reference/src/picohttpparser/picohttpparser.h:51-52
+  http_read_request   /root/reference/src/reactor/http.h:36
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIBRHP = os.path.join(_HERE, "librhp.so")
+LIBHOST = os.path.join(_HERE, "librhp_host.so")
+
+RHP_PAD = 256
+RHP_MAX_LEN = 65535
+RHP_MAX_HEADERS = 64
+RHP_RET_TOOLONG = -3
+RHP_WORK_WORDS = 64
+MODE_PHR, MODE_HTTP = 0, 1
+IMPL_DFA, IMPL_EXACT = 0, 1
+RHP_NAME_NULL = 0xFFFF
+F_EXACT = 0x1
+
+GEN_TFB128, GEN_GET256, GEN_ZIPF, GEN_POST1K, GEN_FUZZ, GEN_FUZZ_HTTP = 1, 2, 3, 5, 100, 101
+
+# numpy views of the C records (rhp.h)
+REQ_DTYPE = np.dtype([("ret", "<i4"), ("method_len", "<u2"), ("path_off", "<u2"), ("path_len", "<u2"),
+                      ("method_off", "u1"), ("minor_version", "i1"), ("num_headers", "<u2"),
+                      ("flags", "<u2")])
+HDR_DTYPE = np.dtype([("name_off", "<u2"), ("name_len", "<u2"), ("value_off", "<u2"), ("value_len", "<u2")])
+HTTP_DTYPE = np.dtype([("result", "<i4"), ("body_kind", "<u4"), ("consumed", "<u8"), ("body_len", "<u8")])
+assert REQ_DTYPE.itemsize == 16 and HDR_DTYPE.itemsize == 8 and HTTP_DTYPE.itemsize == 24
+
+
+class Batch(ctypes.Structure):
+    """struct rhp_batch (include/rhp.h)."""
+    _fields_ = [("bytes", ctypes.c_void_p), ("bytes_rw", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
+                ("bytes_size", ctypes.c_uint64), ("n", ctypes.c_uint32), ("max_headers", ctypes.c_uint32),
+                ("mode", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("reqs", ctypes.c_void_p),
+                ("hdrs", ctypes.c_void_p), ("http", ctypes.c_void_p), ("work", ctypes.c_void_p)]
+
+
+# exported C-ABI symbols of librhp.so, as declared in include/rhp.h
+RHP_SYMBOLS = ("rhp_parse_batch", "rhp_set_impl", "rhp_kernel_name", "rhp_version")
+HOST_SYMBOLS = ("rhp_gen_size", "rhp_gen_fill", "rhp_gen_header_bytes", "rhp_splitmix64",
+                "rhp_emu_parse_batch", "rhp_cpu_parse_batch")
+
+_rhp = None
+_host = None
+
+
+def lib() -> ctypes.CDLL:
+    """librhp.so (HIP).  Raises if it is missing: there is no fallback."""
+    global _rhp
+    if _rhp is None:
+        if not os.path.exists(LIBRHP):
+            raise RuntimeError(f"{LIBRHP} missing: run __graft_entry__.build() (hipcc gfx950)")
+        _rhp = ctypes.CDLL(LIBRHP)
+        _rhp.rhp_parse_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p]
+        _rhp.rhp_parse_batch.restype = ctypes.c_int
+        _rhp.rhp_set_impl.argtypes = [ctypes.c_int]
+        _rhp.rhp_set_impl.restype = ctypes.c_int
+        _rhp.rhp_kernel_name.restype = ctypes.c_char_p
+        _rhp.rhp_version.restype = ctypes.c_char_p
+    return _rhp
+
+
+def host() -> ctypes.CDLL:
+    """librhp_host.so: generator, CPU exact parser, DFA emulator."""
+    global _host
+    if _host is None:
+        if not os.path.exists(LIBHOST):
+            raise RuntimeError(f"{LIBHOST} missing: run __graft_entry__.build()")
+        _host = ctypes.CDLL(LIBHOST)
+        u64 = ctypes.c_uint64
+        _host.rhp_gen_size.argtypes = [ctypes.c_int, u64, u64, u64]
+        _host.rhp_gen_size.restype = u64
+        _host.rhp_gen_fill.argtypes = [ctypes.c_int, u64, u64, u64, ctypes.c_void_p, ctypes.c_void_p]
+        _host.rhp_gen_fill.restype = ctypes.c_int
+        _host.rhp_gen_header_bytes.argtypes = [ctypes.c_int, u64, u64, u64]
+        _host.rhp_gen_header_bytes.restype = u64
+        _host.rhp_emu_parse_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p]
+        _host.rhp_emu_parse_batch.restype = ctypes.c_int
+        _host.rhp_cpu_parse_batch.argtypes = [ctypes.POINTER(Batch)]
+        _host.rhp_cpu_parse_batch.restype = ctypes.c_int
+    return _host
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def generate(config: int, n: int, seed: int, lo: int = 0):
+    """Requests [lo, lo+n) of a generator config -> (bytes uint8[size+RHP_PAD], offsets uint64[n+1])."""
+    h = host()
+    size = h.rhp_gen_size(config, lo, lo + n, seed)
+    if size == 0 and n > 0 and config not in (GEN_FUZZ, GEN_FUZZ_HTTP):
+        raise ValueError(f"bad generator config {config}")
+    buf = np.zeros(size + RHP_PAD, dtype=np.uint8)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    if h.rhp_gen_fill(config, lo, lo + n, seed, _ptr(buf), _ptr(off)) != 0:
+        raise ValueError(f"generator failed for config {config}")
+    return buf, off
+
+
+def header_bytes(config: int, n: int, seed: int, lo: int = 0) -> int:
+    """Algorithmic bytes of requests [lo, lo+n)."""
+    return int(host().rhp_gen_header_bytes(config, lo, lo + n, seed))
+
+
+@dataclass
+class Result:
+    reqs: np.ndarray           # REQ_DTYPE [n]
+    hdrs: np.ndarray           # HDR_DTYPE [n, max_headers]
+    http: np.ndarray | None    # HTTP_DTYPE [n] (http mode)
+    bytes_out: np.ndarray | None = None  # request bytes after http mode (chunked bodies rewritten)
+
+
+def _host_batch(buf, off, max_headers, mode):
+    n = len(off) - 1
+    reqs = np.zeros(n, dtype=REQ_DTYPE)
+    hdrs = np.zeros((n, max(max_headers, 1)), dtype=HDR_DTYPE)
+    http = np.zeros(n, dtype=HTTP_DTYPE)
+    rw = buf.copy()
+    b = Batch(_ptr(rw), _ptr(rw), _ptr(off), rw.size, n, max_headers, mode, 0, _ptr(reqs), _ptr(hdrs),
+              _ptr(http), 0)
+    return b, Result(reqs, hdrs[:, :max_headers], http if mode == MODE_HTTP else None, rw)
+
+
+def emulate(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR):
+    """Run the kernel's DFA algorithm on the CPU (tests).  Returns (Result, stats[3])."""
+    b, res = _host_batch(buf, off, max_headers, mode)
+    stats = np.zeros(3, dtype=np.uint64)
+    rc = host().rhp_emu_parse_batch(ctypes.byref(b), _ptr(stats))
+    if rc != 0:
+        raise RuntimeError(f"rhp_emu_parse_batch failed: {rc}")
+    return res, stats
+
+
+def parse_cpu_exact(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR):
+    """The product's exact scalar parser on the host (rhp_scalar.h), e.g. for the reactor shim."""
+    b, res = _host_batch(buf, off, max_headers, mode)
+    host().rhp_cpu_parse_batch(ctypes.byref(b))
+    return res
+
+
+class DeviceBatch:
+    """A batch resident in HBM plus its output buffers (torch tensors as plumbing)."""
+
+    def __init__(self, buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,
+                 device: str = "cuda"):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("no GPU visible: the rhp product path runs on MI355X only")
+        self.n = len(off) - 1
+        self.max_headers = max_headers
+        self.mode = mode
+        self.bytes = torch.from_numpy(buf).to(device)
+        self.offsets = torch.from_numpy(off.view(np.int64)).to(device)
+        self.reqs = torch.zeros(self.n * REQ_DTYPE.itemsize, dtype=torch.uint8, device=device)
+        self.hdrs = torch.zeros(max(self.n * max_headers, 1) * HDR_DTYPE.itemsize, dtype=torch.uint8,
+                                device=device)
+        self.http = torch.zeros((self.n if mode == MODE_HTTP else 1) * HTTP_DTYPE.itemsize, dtype=torch.uint8,
+                                device=device)
+        self.work = torch.zeros(RHP_WORK_WORDS, dtype=torch.int32, device=device)
+
+    def desc(self) -> Batch:
+        return Batch(self.bytes.data_ptr(), self.bytes.data_ptr(), self.offsets.data_ptr(), self.bytes.numel(),
+                     self.n, self.max_headers, self.mode, 0, self.reqs.data_ptr(), self.hdrs.data_ptr(),
+                     self.http.data_ptr(), self.work.data_ptr())
+
+    def launch(self, stream=None) -> None:
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        d = self.desc()
+        rc = lib().rhp_parse_batch(ctypes.byref(d), ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"rhp_parse_batch failed: {rc}")
+
+    def result(self) -> Result:
+        import torch
+        torch.cuda.synchronize()
+        reqs = self.reqs.cpu().numpy().view(REQ_DTYPE)
+        hdrs = self.hdrs.cpu().numpy().view(HDR_DTYPE)[: self.n * self.max_headers]
+        hdrs = hdrs.reshape(self.n, self.max_headers)
+        http = self.http.cpu().numpy().view(HTTP_DTYPE) if self.mode == MODE_HTTP else None
+        out = self.bytes.cpu().numpy() if self.mode == MODE_HTTP else None
+        return Result(reqs, hdrs, http, out)
+
+
+def parse_batch(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,
+                impl: int = IMPL_DFA) -> Result:
+    """Parse a host batch on the GPU (copies in, one launch, copies out)."""
+    lib().rhp_set_impl(impl)
+    try:
+        db = DeviceBatch(buf, off, max_headers, mode)
+        db.launch()
+        return db.result()
+    finally:
+        lib().rhp_set_impl(IMPL_DFA)

@@ -1,0 +1,276 @@
+/*
+ * rhp_scalar.h -- exact scalar request parser, compiled for host and device.
+ *
+ * The DFA kernel (rhp_kernel.hip) hands a request to this path when its fast
+ * table cannot decide it alone: the buffer ends before the request completes
+ * (end-of-buffer semantics, including the past-the-end SP skips at
+ * picohttpparser.c:356-362), obs-fold lines, an empty method, a bad version,
+ * non-GET framing in http mode, requests longer than the DFA's capture area.
+ * It is the executable form of the semantics the DFA table is derived from.
+ *
+ * Semantics followed (all /root/reference/...):
+ *   phr_parse_request  src/picohttpparser/picohttpparser.c:71-94,134-195,245-409
+ *   http_read_request  src/reactor/http.c:73-160,167-234; memcasecmp data.c:11-28
+ */
+#ifndef RHP_SCALAR_H
+#define RHP_SCALAR_H
+
+#include <stdint.h>
+#include "rhp.h"
+
+#if defined(__HIPCC__)
+#define RHP_HD __host__ __device__ __forceinline__
+#else
+#define RHP_HD static inline
+#endif
+
+namespace rhp {
+
+enum : int { kBad = -1, kPartial = -2 };
+
+RHP_HD bool is_tchar(uint32_t c)
+{
+  /* token_char_map (picohttpparser.c:96-103) as two 64-bit row masks */
+  const uint64_t lo = 0x03ff6cfa00000000ull;  /* 0x00-0x3f: ! # $ % & ' * + - . 0-9 */
+  const uint64_t hi = 0x57ffffffc7fffffeull;  /* 0x40-0x7f: A-Z ^ _ ` a-z | ~ */
+  if (c >= 128) return false;
+  return ((c < 64 ? lo : hi) >> (c & 63)) & 1u;
+}
+RHP_HD bool is_ctl_del(uint32_t c) { return c < 0x20u || c == 0x7fu; }
+RHP_HD bool is_ows(uint32_t c) { return c == ' ' || c == '\t'; }
+
+/* Parse one request.  b may be read beyond len (batch contract).  Headers are
+ * written to h[0..max).  Returns the phr status; fills r. */
+RHP_HD int scalar_phr(const uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h)
+{
+  uint64_t p = 0;
+  r->method_off = 0; r->method_len = 0; r->path_off = 0; r->path_len = 0;
+  r->minor_version = -1; r->num_headers = 0;
+#define RHP_FAIL(code) do { r->ret = (code); return (code); } while (0)
+#define RHP_EOF() do { if (p == len) RHP_FAIL(kPartial); } while (0)
+#define RHP_CRLF() do { ++p; RHP_EOF(); if (b[p++] != '\n') RHP_FAIL(kBad); } while (0)
+  RHP_EOF();
+  if (b[p] == '\r') RHP_CRLF();
+  else if (b[p] == '\n') ++p;
+
+  uint64_t tok[2][2];              /* [method, path][start, end] */
+  for (int t = 0; t < 2; t++) {
+    tok[t][0] = p;
+    RHP_EOF();
+    for (;;) {
+      uint32_t c = b[p];
+      if (c == ' ') break;
+      if (is_ctl_del(c)) RHP_FAIL(kBad);
+      ++p;
+      RHP_EOF();
+    }
+    tok[t][1] = p;
+    do ++p; while (b[p] == ' ');   /* no EOF test: may run past len */
+  }
+  if (tok[0][1] == tok[0][0] || tok[1][1] == tok[1][0]) RHP_FAIL(kBad);
+  if ((int64_t) len - (int64_t) p < 9) RHP_FAIL(kPartial);
+  const uint8_t *v = b + p;
+  if (v[0] != 'H' || v[1] != 'T' || v[2] != 'T' || v[3] != 'P' || v[4] != '/' || v[5] != '1' ||
+      v[6] != '.' || v[7] < '0' || v[7] > '9')
+    RHP_FAIL(kBad);
+  int minor = v[7] - '0';
+  p += 8;
+  if (b[p] == '\r') RHP_CRLF();
+  else if (b[p] == '\n') ++p;
+  else RHP_FAIL(kBad);
+
+  uint32_t n = 0;
+  for (;;) {
+    RHP_EOF();
+    if (b[p] == '\r') { RHP_CRLF(); break; }
+    if (b[p] == '\n') { ++p; break; }
+    if (n == max) RHP_FAIL(kBad);
+    uint64_t name = p, name_len = 0;
+    bool fold = n != 0 && is_ows(b[p]);
+    if (!fold) {
+      for (;;) {
+        uint32_t c = b[p];
+        if (c == ':') break;
+        if (!is_tchar(c)) RHP_FAIL(kBad);
+        ++p;
+        RHP_EOF();
+      }
+      name_len = p - name;
+      if (name_len == 0) RHP_FAIL(kBad);
+      ++p;
+      for (;; ++p) {
+        RHP_EOF();
+        if (!is_ows(b[p])) break;
+      }
+    }
+    uint64_t vs = p;
+    uint32_t c;
+    for (;; ++p) {
+      RHP_EOF();
+      c = b[p];
+      if ((c < 0x20u && c != '\t') || c == 0x7fu) break;
+    }
+    uint64_t ve = p;
+    if (c == '\r') RHP_CRLF();
+    else if (c == '\n') ++p;
+    else RHP_FAIL(kBad);
+    while (ve > vs && is_ows(b[ve - 1])) --ve;
+    h[n].name_off = fold ? (uint16_t) RHP_NAME_NULL : (uint16_t) name;
+    h[n].name_len = (uint16_t) name_len;
+    h[n].value_off = (uint16_t) vs;
+    h[n].value_len = (uint16_t) (ve - vs);
+    ++n;
+  }
+#undef RHP_CRLF
+#undef RHP_EOF
+#undef RHP_FAIL
+  r->method_off = (uint8_t) tok[0][0];
+  r->method_len = (uint16_t) (tok[0][1] - tok[0][0]);
+  r->path_off = (uint16_t) tok[1][0];
+  r->path_len = (uint16_t) (tok[1][1] - tok[1][0]);
+  r->minor_version = (int8_t) minor;
+  r->num_headers = (uint16_t) n;
+  r->ret = (int32_t) p;
+  return r->ret;
+}
+
+/* ---- http_read_request framing (http.c:177-234) over a parsed request ---- */
+
+RHP_HD uint32_t upper(uint32_t c) { return (c - 'a' < 26u) ? c - 32u : c; }
+
+RHP_HD bool name_eq(const uint8_t *b, const rhp_hdr_t &h, const char *name, uint32_t n)
+{
+  if (h.name_off == RHP_NAME_NULL || h.name_len != n) return false;
+  for (uint32_t i = 0; i < n; i++)
+    if (upper(b[h.name_off + i]) != upper((uint8_t) name[i])) return false;
+  return true;
+}
+
+/* strtoull(s, NULL, 10), glibc C locale (saturating, sign-negated) */
+RHP_HD uint64_t strtoull10(const uint8_t *s)
+{
+  while (*s == ' ' || (*s >= '\t' && *s <= '\r')) s++;
+  bool neg = false;
+  if (*s == '+' || *s == '-') neg = *s++ == '-';
+  uint64_t v = 0;
+  bool ovf = false;
+  for (; *s >= '0' && *s <= '9'; s++) {
+    uint64_t d = *s - '0';
+    ovf |= v > (~0ull - d) / 10;
+    v = v * 10 + d;
+  }
+  return ovf ? ~0ull : neg ? 0 - v : v;
+}
+
+RHP_HD int hexval(uint32_t c)
+{
+  if (c - '0' < 10u) return (int) (c - '0');
+  if ((c | 0x20u) - 'a' < 6u) return (int) ((c | 0x20u) - 'a' + 10);
+  return -1;
+}
+
+/* http_chunk_size + http_chunk (http.c:73-132): >0 bytes of this chunk
+ * (size line + data + 2), 0 need more, -1 malformed; *data_off / *data_len */
+RHP_HD int64_t one_chunk(const uint8_t *in, uint64_t size, uint64_t *data_off, uint64_t *data_len)
+{
+  uint64_t nl = 0;
+  while (nl < size && in[nl] != '\n') nl++;
+  if (nl == size) return 0;                      /* no '\n' yet */
+  const uint8_t *p = in;
+  while (is_ows(*p)) p++;
+  const uint8_t *digits = p;
+  while (hexval(*p) >= 0) p++;
+  if (p == digits) return -1;
+  while (is_ows(*p)) p++;
+  if (*p == ';') {
+    while (*p != '\n') p++;
+    if (p[-1] != '\r') return -1;
+  } else {
+    if (*p != '\r') return -1;
+    p++;
+  }
+  if (*p != '\n') return -1;
+  p++;
+  uint64_t cs = 0;
+  bool ovf = false;
+  for (const uint8_t *q = digits; hexval(*q) >= 0; q++) {
+    ovf |= (cs >> 60) != 0;
+    cs = (cs << 4) | (uint64_t) hexval(*q);
+  }
+  if (ovf || cs == ~0ull) return -1;             /* strtoul == ULONG_MAX */
+  uint64_t n = (uint64_t) (p - in);
+  if (n + 2 > size) return 0;
+  if (cs > size - n - 2) return 0;
+  *data_off = n;
+  *data_len = cs;
+  return (int64_t) (cs + n + 2);
+}
+
+/* http_dechunk (http.c:134-160): validate, then compact payloads in place */
+RHP_HD int64_t dechunk(uint8_t *in, uint64_t size, uint64_t *body_len)
+{
+  uint64_t off = 0, doff = 0, dlen = 0;
+  do {
+    int64_t n = one_chunk(in + off, size - off, &doff, &dlen);
+    if (n <= 0) return n;
+    off += (uint64_t) n;
+  } while (dlen);
+  uint64_t total = 0;
+  off = 0;
+  do {
+    int64_t n = one_chunk(in + off, size - off, &doff, &dlen);
+    const uint8_t *src = in + off + doff;
+    for (uint64_t i = 0; i < dlen; i++) in[total + i] = src[i];  /* dst <= src: forward copy */
+    off += (uint64_t) n;
+    total += dlen;
+  } while (dlen);
+  *body_len = total;
+  return (int64_t) off;
+}
+
+/* Framing decision given a successful phr parse (n = r.ret > 0). */
+RHP_HD void http_frame(uint8_t *b, uint64_t len, const rhp_req_t &r, const rhp_hdr_t *h, rhp_http_t *x)
+{
+  const int64_t n = r.ret;
+  x->result = 1; x->body_kind = 0; x->consumed = (uint64_t) n; x->body_len = 0;
+  if (r.method_len == 3 && b[r.method_off] == 'G' && b[r.method_off + 1] == 'E' && b[r.method_off + 2] == 'T')
+    return;                                       /* GET fast path (http.c:198-202) */
+  int te = -1, cl = -1;
+  for (uint32_t i = 0; i < r.num_headers; i++) {
+    if (te < 0 && name_eq(b, h[i], "Transfer-Encoding", 17)) te = (int) i;
+    if (cl < 0 && name_eq(b, h[i], "Content-Length", 14)) cl = (int) i;
+  }
+  bool te_set = te >= 0 && h[te].value_len != 0;
+  bool cl_set = cl >= 0 && h[cl].value_len != 0;
+  if (cl_set) {
+    if (te_set) { x->result = -1; x->consumed = 0; return; }
+    uint64_t size = strtoull10(b + h[cl].value_off);
+    if (len < (uint64_t) n + size) { x->result = 0; x->consumed = 0; return; }
+    x->body_kind = 1; x->body_len = size; x->consumed = (uint64_t) n + size;
+    return;
+  }
+  if (te_set) {
+    const char *ch = "CHUNKED";
+    bool eq = h[te].value_len == 7;
+    for (uint32_t i = 0; eq && i < 7; i++) eq = upper(b[h[te].value_off + i]) == (uint32_t) ch[i];
+    if (!eq) { x->result = -1; x->consumed = 0; return; }
+    uint64_t blen = 0;
+    int64_t size = dechunk(b + n, len - (uint64_t) n, &blen);
+    if (size <= 0) { x->result = (int32_t) size; x->consumed = 0; return; }
+    x->body_kind = 1; x->body_len = blen; x->consumed = (uint64_t) n + (uint64_t) size;
+  }
+}
+
+/* Whole http_read_request for one request. */
+RHP_HD void scalar_http(uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, rhp_http_t *x)
+{
+  int n = scalar_phr(b, len, max, r, h);
+  x->body_kind = 0; x->consumed = 0; x->body_len = 0;
+  if (len == 0) { x->result = 0; return; }
+  if (n <= 0) { x->result = n == kBad ? -1 : 0; return; }
+  http_frame(b, len, *r, h, x);
+}
+
+}  // namespace rhp
+
+#endif

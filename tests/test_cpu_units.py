@@ -1,0 +1,135 @@
+"""CPU: generator determinism and sharding, library exports, DFA emulation fuzz
+against the oracle, edge cases of the batch contract."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import libreactorng_amd as rhp
+from oracle_util import assert_same, canon, run_oracle, to_rhp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions(header):
+    text = open(os.path.join(ROOT, "include", header)).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(rhp_[a-z_0-9]+)\s*\(", text, re.M)))
+
+
+def exported(path):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", path], text=True)
+    return {line.split()[-1] for line in out.splitlines() if " T " in line}
+
+
+def test_librhp_exports_every_declared_symbol():
+    decl = declared_functions("rhp.h")
+    assert set(decl) == set(rhp.RHP_SYMBOLS), decl
+    have = exported(rhp.LIBRHP)
+    missing = [s for s in decl if s not in have]
+    assert not missing, missing
+    lib = rhp.lib()           # loads without a GPU; no compute call here
+    assert lib.rhp_version().startswith(b"rhp")
+    assert lib.rhp_set_impl(7) == -22 and lib.rhp_set_impl(0) == 0
+
+
+def test_host_lib_exports():
+    decl = declared_functions("rhp_gen.h")
+    have = exported(rhp.LIBHOST)
+    assert not [s for s in decl if s not in have]
+    for s in rhp.HOST_SYMBOLS:
+        assert s in have, s
+
+
+def test_parse_batch_argument_errors_without_gpu():
+    lib = rhp.lib()
+    assert lib.rhp_parse_batch(None, None) == -22
+    b = rhp.Batch()
+    assert lib.rhp_parse_batch(ctypes.byref(b), None) == -22      # null pointers rejected
+
+
+@pytest.mark.parametrize("cfg", [1, 2, 3, 5, 100, 101])
+def test_generator_deterministic_and_shardable(cfg):
+    a, oa = rhp.generate(cfg, 300, 42)
+    b, ob = rhp.generate(cfg, 300, 42)
+    assert np.array_equal(a, b) and np.array_equal(oa, ob)
+    assert np.all(a[int(oa[-1]):] == 0) and len(a) - int(oa[-1]) == rhp.RHP_PAD
+    s, os_ = rhp.generate(cfg, 100, 42, lo=120)
+    assert bytes(s[: int(os_[-1])]) == bytes(a[int(oa[120]):int(oa[220])])
+    assert np.array_equal(os_, oa[120:221] - oa[120])
+
+
+def test_config_shapes():
+    buf, off = rhp.generate(rhp.GEN_GET256, 64, 0x5EED0002)
+    assert np.all(np.diff(off) == 256)
+    buf, off = rhp.generate(rhp.GEN_POST1K, 2000, 0x5EED0005)
+    assert np.all(np.diff(off) == 1024)
+    hb = rhp.header_bytes(rhp.GEN_POST1K, 2000, 0x5EED0005)
+    assert 2000 * 128 < hb < 2000 * 170
+    buf, off = rhp.generate(rhp.GEN_ZIPF, 20000, 0x5EED0003)
+    lens = np.diff(off)
+    assert lens.min() >= 18 and lens.max() <= 4096
+    assert 500 < lens.mean() < 800   # mean ~642 B
+
+
+@pytest.mark.parametrize("seed", [101, 202, 303])
+@pytest.mark.parametrize("maxh", [0, 1, 5, 16, 64])
+def test_dfa_emulation_fuzz_vs_oracle(seed, maxh):
+    for cfg, mode in ((rhp.GEN_FUZZ, rhp.MODE_PHR), (rhp.GEN_FUZZ_HTTP, rhp.MODE_HTTP)):
+        buf, off = rhp.generate(cfg, 6000, seed + maxh)
+        res, stats = rhp.emulate(buf, off, maxh, mode)
+        want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
+        assert_same(canon(res, mode), want, buf, off, f"emu cfg{cfg} seed{seed} maxh{maxh}")
+
+
+def pack(reqs, pad=rhp.RHP_PAD, align_shift=0):
+    parts = [bytes(r) for r in reqs]
+    off = np.zeros(len(parts) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(p) for p in parts])
+    off += align_shift
+    buf = np.zeros(int(off[-1]) + pad, dtype=np.uint8)
+    buf[align_shift:int(off[-1])] = np.frombuffer(b"".join(parts), dtype=np.uint8)
+    return buf, off
+
+
+EDGE = [
+    b"", b"G", b"GET", b"GET ", b"GET  ", b" ", b"GET /", b"GET / ", b"\r", b"\n", b"\r\n", b"\r\nGET ",
+    b"GET / HTTP/1.1\r\n\r\n", b"GET / HTTP/1.1\n\n", b"\r\nGET / HTTP/1.1\r\n\r\n", b"\nGET / HTTP/1.0\n\n",
+    b"GET / HTTP/1.10\r\n\r\n", b"GET / HTTP/1.1\r\nA: b\r\n \tfolded  \r\n\r\n", b"GET / HTTP/1.1\r\nA :b\r\n\r\n",
+    b"GET / HTTP/1.1\r\n:b\r\n\r\n", b"GET / HTTP/1.1\r\nA:\r\n\r\n", b"GET / HTTP/1.1\r\nA: \t \r\n\r\n",
+    b"GET / HTTP/1.1\r\nA: x \t\r\n\r\n", b"GET / HTTP/1.1\r\nA: \x80\xff \r\n\r\n", b"GET / HTTP/1.1\r\nA: a\rb\r\n\r\n",
+    b"GET / HTTP/1.1\r\nA: a\x7fb\r\n\r\n", b"GET \x80\xfe HTTP/1.1\r\n\r\n", b"\x80 / HTTP/1.1\r\n\r\n",
+    b"GET / HTTP/1.1\r\n\r\nGET / HTTP/1.1\r\n\r\n", b"POST / HTTP/1.1\r\nContent-Length: 3\r\n\r\nabc",
+    b"GET / HTTP/1.1\r", b"GET / HTTP/1.1\r\nA: b\r", b"GET / HTTP/1.1\r\nA: b\r\n\r",
+    b"  / HTTP/1.1\r\n\r\n", b"GET  /  HTTP/1.1\r\n\r\n", b"GET / H\r\n\r\n",
+]
+
+
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+@pytest.mark.parametrize("maxh", [0, 1, 16])
+def test_edge_cases_emulation(shift, maxh):
+    buf, off = pack(EDGE, align_shift=shift)
+    for mode in (rhp.MODE_PHR, rhp.MODE_HTTP):
+        res, _ = rhp.emulate(buf, off, maxh, mode)
+        want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
+        assert_same(canon(res, mode), want, buf, off, f"edge shift{shift} maxh{maxh} mode{mode}")
+
+
+def test_max_headers_boundary():
+    """17 headers with capacity 16 -> -1; exactly 16 -> ok."""
+    def req(k):
+        return b"GET / HTTP/1.1\r\n" + b"".join(b"H%d: v\r\n" % i for i in range(k)) + b"\r\n"
+    buf, off = pack([req(15), req(16), req(17), req(40)])
+    res, _ = rhp.emulate(buf, off, 16)
+    assert list(res.reqs["ret"][:2] > 0) == [True, True] and list(res.reqs["ret"][2:]) == [-1, -1]
+    want = to_rhp(*run_oracle(buf, off, 16)[:3], rhp.MODE_PHR)
+    assert_same(canon(res, rhp.MODE_PHR), want, buf, off, "max headers")
+
+
+def test_toolong_request_reported():
+    big = b"GET /" + b"a" * 70000 + b" HTTP/1.1\r\n\r\n"
+    buf, off = pack([b"GET / HTTP/1.1\r\n\r\n", big])
+    res, _ = rhp.emulate(buf, off, 16)
+    assert res.reqs["ret"][0] == 18 and res.reqs["ret"][1] == rhp.RHP_RET_TOOLONG

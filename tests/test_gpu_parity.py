@@ -1,0 +1,122 @@
+"""GPU parity: the HIP kernels (through the C-ABI in librhp.so) against the
+reference's golden fixtures and the oracle, bit-exact, at fixture sizes and at
+BASELINE.json full sizes."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import libreactorng_amd as rhp
+from oracle_util import assert_same, canon, run_oracle, to_rhp
+from test_cpu_units import EDGE, pack
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))["sets"]
+
+
+def golden(name):
+    spec = MANIFEST[name]
+    buf, off = rhp.generate(spec["config"], spec["n"], spec["seed"])
+    assert hashlib.sha256(buf.tobytes()).hexdigest() == spec["input_sha256"]
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    return spec, buf, off, (z["reqs"], z["hdrs"], z["http"] if "http" in z.files else None), z
+
+
+@pytest.mark.parametrize("impl", [rhp.IMPL_DFA, rhp.IMPL_EXACT])
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_gpu_matches_reference_golden(name, impl):
+    spec, buf, off, want, z = golden(name)
+    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], impl=impl)
+    assert_same(canon(res, spec["mode"]), want, buf, off, f"GPU impl{impl} vs golden {name}")
+    if "bytes_out_sha256" in z.files:
+        assert hashlib.sha256(res.bytes_out.tobytes()).digest() == z["bytes_out_sha256"].tobytes()
+
+
+def test_gpu_reference_http_vectors():
+    spec = json.load(open(os.path.join(GOLDEN, "http_request_tests.json")))
+    for v in spec["vectors"]:
+        s = v["request"].encode("latin-1")
+        buf, off = pack([s])
+        res = rhp.parse_batch(buf, off, 16, rhp.MODE_HTTP)
+        result, consumed = int(res.http["result"][0]), int(res.http["consumed"][0])
+        remaining = len(s) - consumed if result == 1 else len(s)
+        assert (result, remaining) == (v["result"], v["remaining"]), v
+
+
+@pytest.mark.parametrize("maxh", [0, 1, 3, 16, 32, 64])
+def test_gpu_fuzz_vs_oracle(maxh):
+    for cfg, mode, seed in ((rhp.GEN_FUZZ, rhp.MODE_PHR, 9000 + maxh), (rhp.GEN_FUZZ_HTTP, rhp.MODE_HTTP, 9100 + maxh)):
+        buf, off = rhp.generate(cfg, 60000, seed)
+        res = rhp.parse_batch(buf, off, maxh, mode)
+        want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
+        assert_same(canon(res, mode), want, buf, off, f"GPU fuzz cfg{cfg} maxh{maxh}")
+        # the DFA must decide most requests itself (the exact path is the rare path)
+        assert (res.reqs["flags"] & rhp.F_EXACT).mean() < 0.35
+
+
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+def test_gpu_edge_cases(shift):
+    buf, off = pack(EDGE * 3, align_shift=shift)
+    for maxh in (0, 1, 16):
+        for mode in (rhp.MODE_PHR, rhp.MODE_HTTP):
+            res = rhp.parse_batch(buf, off, maxh, mode)
+            want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
+            assert_same(canon(res, mode), want, buf, off, f"GPU edge shift{shift} maxh{maxh} mode{mode}")
+
+
+def test_gpu_toolong_and_empty_batch():
+    big = b"GET /" + b"a" * 70000 + b" HTTP/1.1\r\n\r\n"
+    buf, off = pack([b"GET / HTTP/1.1\r\n\r\n", big, b""])
+    res = rhp.parse_batch(buf, off, 16)
+    assert list(res.reqs["ret"]) == [18, rhp.RHP_RET_TOOLONG, -2]
+    buf, off = pack([])
+    res = rhp.parse_batch(buf, off, 16)
+    assert len(res.reqs) == 0
+
+
+def test_gpu_repeated_launches_rearm_work_counter():
+    buf, off = rhp.generate(rhp.GEN_ZIPF, 5000, 77)
+    db = rhp.DeviceBatch(buf, off, 32)
+    want = to_rhp(*run_oracle(buf, off, 32)[:3], rhp.MODE_PHR)
+    for _ in range(5):
+        db.reqs.zero_()
+        db.launch()
+        assert_same(canon(db.result(), rhp.MODE_PHR), want, buf, off, "relaunch")
+
+
+def test_gpu_full_size_config2_properties():
+    """BASELINE config 2 at full size (1M x 256 B): every record equals the template
+    answer shifted by the 138 B path; a 64K slice compared against the oracle."""
+    n = 1 << 20
+    buf, off = rhp.generate(rhp.GEN_GET256, n, 0x5EED0002)
+    res = rhp.parse_batch(buf, off, 16)
+    r = res.reqs
+    assert np.all(r["ret"] == 256) and np.all(r["path_off"] == 4) and np.all(r["path_len"] == 138)
+    assert np.all(r["method_len"] == 3) and np.all(r["minor_version"] == 1) and np.all(r["num_headers"] == 4)
+    assert np.all(r["flags"] == 0)
+    h = res.hdrs[:, :4]
+    kat = [(25, 4, 31, 15), (48, 6, 56, 10), (68, 10, 80, 10), (92, 10, 104, 20)]
+    for k, (no, nl, vo, vl) in enumerate(kat):
+        assert np.all(h[:, k]["name_off"] == no + 128) and np.all(h[:, k]["name_len"] == nl)
+        assert np.all(h[:, k]["value_off"] == vo + 128) and np.all(h[:, k]["value_len"] == vl)
+    lo, hi = n - 65536, n
+    s, so = rhp.generate(rhp.GEN_GET256, hi - lo, 0x5EED0002, lo=lo)
+    want = to_rhp(*run_oracle(s, so, 16)[:3], rhp.MODE_PHR)
+    got = canon(rhp.Result(r[lo:hi], res.hdrs[lo:hi], None), rhp.MODE_PHR)
+    assert_same(got, want, s, so, "config 2 tail slice")
+
+
+@pytest.mark.parametrize("cfg,maxh,mode", [(rhp.GEN_ZIPF, 32, rhp.MODE_PHR), (rhp.GEN_ZIPF, 16, rhp.MODE_PHR),
+                                           (rhp.GEN_POST1K, 16, rhp.MODE_HTTP)])
+def test_gpu_full_size_configs_vs_oracle(cfg, maxh, mode):
+    """BASELINE configs 3 and 5 at full size (1M requests), bit-exact vs the oracle."""
+    n = 1 << 20
+    seed = {rhp.GEN_ZIPF: 0x5EED0003, rhp.GEN_POST1K: 0x5EED0005}[cfg]
+    buf, off = rhp.generate(cfg, n, seed)
+    res = rhp.parse_batch(buf, off, maxh, mode)
+    want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
+    assert_same(canon(res, mode), want, buf, off, f"full size cfg{cfg} maxh{maxh}")

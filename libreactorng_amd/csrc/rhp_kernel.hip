@@ -343,13 +343,14 @@ int rhp_set_impl(int impl)
 
 int rhp_parse_batch(const rhp_batch_t *b, void *stream)
 {
-  if (!b || !b->bytes || !b->offsets || !b->reqs || !b->work) return -22;
+  if (!b) return -22;
+  if (b->n == 0) return 0;                       /* nothing to parse, nothing touched */
+  if (!b->bytes || !b->offsets || !b->reqs || !b->work) return -22;
   if (b->max_headers > RHP_MAX_HEADERS) return -22;
   if (b->max_headers > 0 && !b->hdrs) return -22;
   if (b->mode == RHP_MODE_HTTP && (!b->http || !b->bytes_rw)) return -22;
   if (b->mode != RHP_MODE_PHR && b->mode != RHP_MODE_HTTP) return -22;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (b->n == 0) return 0;
   if (g_cus == 0) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);

@@ -47,7 +47,14 @@ def test_parse_batch_argument_errors_without_gpu():
     lib = rhp.lib()
     assert lib.rhp_parse_batch(None, None) == -22
     b = rhp.Batch()
+    assert lib.rhp_parse_batch(ctypes.byref(b), None) == 0        # n == 0: nothing to do
+    b.n = 5
     assert lib.rhp_parse_batch(ctypes.byref(b), None) == -22      # null pointers rejected
+    b.n, b.bytes, b.offsets, b.reqs, b.work, b.hdrs = 5, 1, 1, 1, 1, 1
+    b.max_headers = rhp.RHP_MAX_HEADERS + 1
+    assert lib.rhp_parse_batch(ctypes.byref(b), None) == -22      # capacity limit
+    b.max_headers, b.mode = 16, 7
+    assert lib.rhp_parse_batch(ctypes.byref(b), None) == -22      # unknown mode
 
 
 @pytest.mark.parametrize("cfg", [1, 2, 3, 5, 100, 101])

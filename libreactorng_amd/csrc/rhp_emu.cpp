@@ -71,7 +71,9 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
     if (len > RHP_MAX_LEN - 256) s0 = S_SLOW;
     uint32_t st = entry(s0, C_NONE_RL);
     uint32_t cap = cap0;
-    memset(area.data(), 0, cap_lane);
+    /* stale garbage everywhere except the VE slots: the kernel only re-zeroes VE */
+    memset(area.data(), 0xA5, cap_lane);
+    for (uint32_t a = kRlBytes + C_VE; a + 2 <= cap_lane; a += kHdrBytes) st16(a, 0);
     /* blocks until terminal or past the end (block boundary checks) */
     for (;;) {
       if (is_terminal_row(entry_next(st)) || pos >= (int32_t) len) break;

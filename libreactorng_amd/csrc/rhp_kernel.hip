@@ -18,6 +18,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "rhp.h"
@@ -177,9 +178,13 @@ __device__ void finalize(const Params &p, uint32_t i, uint64_t off, uint64_t len
  * The DFA kernel.  One workgroup = WAVES waves; dynamic LDS = table + per-lane
  * capture areas.  Persistent: grid = workgroups resident on the device.
  */
-template <int WAVES>
+template <int WAVES, int FLAGS>
 __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
 {
+  /* FLAGS bit 0: prefetch the next 64-byte window while the current one is parsed
+   * FLAGS bit 1: odd-dword capture stride (conflict-free LDS capture writes) */
+  constexpr bool kPrefetch = FLAGS & 1;
+  constexpr bool kOddStride = FLAGS & 2;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
@@ -206,6 +211,9 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
   uint32_t req = 0;
   uint64_t off = 0, len = 0;
   const uint8_t *win = p.bytes;
+
+  bool fresh = false;                 /* lane got a new request at this boundary */
+  u32x4 wn[4] = {u32x4{0, 0, 0, 0}, u32x4{0, 0, 0, 0}, u32x4{0, 0, 0, 0}, u32x4{0, 0, 0, 0}};
 
   /* wave-uniform pool of requests */
   uint32_t pool_next = 0, pool_end = 0;
@@ -245,7 +253,13 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
         if (len > kFastMaxLen) s0 = S_SLOW;
         st = entry(s0, C_NONE_RL);
         cap = cap0;
-        for (uint32_t b = 0; b < p.cap_lane; b += 16) lds_store_u32x4(cap0 + b, u32x4{0, 0, 0, 0});
+        if (kOddStride) {
+          /* only the VE slots must start at 0 (rhp_dfa.h) */
+          for (uint32_t b = kRlBytes + C_VE; b + 2 <= p.cap_lane; b += kHdrBytes) lds_store_u16(cap0 + b, 0);
+        } else {
+          for (uint32_t b = 0; b < p.cap_lane; b += 16) lds_store_u32x4(cap0 + b, u32x4{0, 0, 0, 0});
+        }
+        fresh = true;
       }
       uint32_t k = (uint32_t) __popcll(idle);
       pool_next += min(k, avail);
@@ -255,8 +269,16 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
 
     /* ---- one 64-byte block: 4 sub-blocks of 16 steps ---- */
     u32x4 w[4];
+    if (kPrefetch) {
 #pragma unroll
-    for (int q = 0; q < 4; q++) w[q] = has ? load_window16(win + 16 * q) : u32x4{0, 0, 0, 0};
+      for (int q = 0; q < 4; q++) w[q] = fresh ? load_window16(win + 16 * q) : wn[q];
+#pragma unroll
+      for (int q = 0; q < 4; q++) wn[q] = has ? load_window16(win + 64 + 16 * q) : u32x4{0, 0, 0, 0};
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; q++) w[q] = has ? load_window16(win + 16 * q) : u32x4{0, 0, 0, 0};
+    }
+    fresh = false;
 
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -305,25 +327,47 @@ __global__ __launch_bounds__(256) void rhp_exact_kernel(Params p)
 namespace {
 int g_impl = RHP_IMPL_DFA;
 int g_cus = 0;
+int g_flags = -1;   /* RHP_DFA_FLAGS (experiments); default below */
 
-template <int WAVES>
+int dfa_flags()
+{
+  if (g_flags < 0) {
+    const char *e = getenv("RHP_DFA_FLAGS");
+    g_flags = e ? (atoi(e) & 3) : 3;
+  }
+  return g_flags;
+}
+
+template <int FLAGS>
+int launch_waves(int waves, const Params &prm, size_t lds, hipStream_t s)
+{
+  switch (waves) {
+  case 8: return launch_dfa<8, FLAGS>(prm, lds, s);
+  case 4: return launch_dfa<4, FLAGS>(prm, lds, s);
+  case 2: return launch_dfa<2, FLAGS>(prm, lds, s);
+  default: return launch_dfa<1, FLAGS>(prm, lds, s);
+  }
+}
+
+template <int WAVES, int FLAGS>
 int launch_dfa(const Params &prm, size_t lds_bytes, hipStream_t s)
 {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES, FLAGS>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return (int) e;
     attr_set = true;
   }
   int per_cu = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rhp_dfa_kernel<WAVES>, WAVES * 64, lds_bytes);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rhp_dfa_kernel<WAVES, FLAGS>, WAVES * 64,
+                                                               lds_bytes);
   if (e != hipSuccess) return (int) e;
   if (per_cu < 1) per_cu = 1;
   uint32_t grid = (uint32_t) (g_cus * per_cu);
   uint32_t need = (prm.n + 64 * WAVES - 1) / (64 * WAVES);
   if (grid > need) grid = need > 0 ? need : 1;
-  hipLaunchKernelGGL(rhp_dfa_kernel<WAVES>, dim3(grid), dim3(WAVES * 64), lds_bytes, s, prm);
+  hipLaunchKernelGGL((rhp_dfa_kernel<WAVES, FLAGS>), dim3(grid), dim3(WAVES * 64), lds_bytes, s, prm);
   return (int) hipGetLastError();
 }
 }  // namespace
@@ -368,7 +412,9 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.n = b->n;
   prm.max_headers = b->max_headers;
   prm.mode = b->mode;
+  const int flags = dfa_flags();
   prm.cap_lane = (cap_bytes(b->max_headers) + 15u) & ~15u;
+  if (flags & 2) prm.cap_lane += 4;      /* odd number of dwords: lanes hit distinct banks */
 
   if (g_impl == RHP_IMPL_EXACT) {
     uint32_t grid = (b->n + 255) / 256;
@@ -381,11 +427,11 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   for (int waves = 8; waves >= 1; waves >>= 1) {
     size_t lds = kTableBytes + waves * per_wave;
     if (lds > budget) continue;
-    switch (waves) {
-    case 8: return launch_dfa<8>(prm, lds, s);
-    case 4: return launch_dfa<4>(prm, lds, s);
-    case 2: return launch_dfa<2>(prm, lds, s);
-    default: return launch_dfa<1>(prm, lds, s);
+    switch (flags) {
+    case 0: return launch_waves<0>(waves, prm, lds, s);
+    case 1: return launch_waves<1>(waves, prm, lds, s);
+    case 2: return launch_waves<2>(waves, prm, lds, s);
+    default: return launch_waves<3>(waves, prm, lds, s);
     }
   }
   return -12;

@@ -18,7 +18,7 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIBRHP = os.path.join(_HERE, "librhp.so")
+LIBRHP = os.environ.get("RHP_LIB", os.path.join(_HERE, "librhp.so"))  # RHP_LIB: A/B experiments only
 LIBHOST = os.path.join(_HERE, "librhp_host.so")
 
 RHP_PAD = 256

@@ -1,78 +1,93 @@
 /*
- * rhp_dfa.h -- the byte DFA that the MI355X kernel runs, one request per lane.
+ * rhp_dfa.h -- the byte DFA that the MI355X kernel runs, one request per lane,
+ * and the event decoder that turns its output into phr_parse_request records.
  *
- * The table re-expresses phr_parse_request (picohttpparser.c:341-409) as a
- * transition table over (state, byte) whose u32 entries carry everything one
- * step needs, so a step is: entry = T[row(entry) + 4*byte] (one LDS read), plus
- * one LDS u16 write that records the byte position into a per-lane capture slot.
+ * The table re-expresses phr_parse_request (picohttpparser.c:341-409, headers
+ * :263-339) as u16 entries over (state, byte): an entry is the LDS byte offset
+ * of the next state's row, so one step is  e = T[e + 2*byte]  (one ds_read_u16).
  *
- *   entry bits  0..15  LDS byte offset of the next state's row
- *   entry bits 16..23  capture slot, byte offset from the lane's capture pointer
- *   entry bits 24..31  capture pointer increment (a new header record starts)
+ * Events.  Rows live in two LDS ranges: plain rows below kEventRow and event
+ * rows at/above it, so bit 14 of an entry says "this transition is an event".
+ * The kernel ORs that bit into a 64-bit per-block mask (two VALU ops per step,
+ * no LDS write) and decodes the mask once per 64-byte block.  For a request the
+ * fast path accepts, the event sequence is fixed by the grammar:
  *
- * The DFA only decides what it can decide without knowing where the buffer
- * ends: every result is trusted only if the deciding byte lies before `len`
- * (the kernel checks), and paths whose reference behaviour depends on the end
- * of the buffer or that are rare (empty method, bad version literal, obs-fold
- * continuation lines) go to the SLOW terminal and are re-parsed by the exact
- * scalar path (rhp_scalar.h).  Both are checked against the oracle.
+ *   ME  PS  PE  RL          request line: method end (1st SP), path start,
+ *                           path end (2nd SP), RL = the CR of "HTTP/1.0\r\n"
+ *                           or the LF of "HTTP/1.1\r\n" (so the position
+ *                           encodes the minor version: RL - PE = 9 or 10)
+ *   { CO  VS  EOL }*        per header line: colon, value start (first
+ *                           non-OWS byte after the colon, the CR for an empty
+ *                           value), the LF that ends the line
+ *   T                       terminal: the final LF (DONE) or the byte at which
+ *                           the reference returns -1 (ERR)
  *
- * Per-lane capture area (u16 positions, relative to the request start):
- *   request line record at cap0 (16 B): MS ME PS PE VD . TERM .
- *     MS/ME method start/end  PS/PE path start/end  VD version digit
- *   header record h at cap0 + 16 + 8h (8 B): LS CO VS VE
- *     LS line start (name)  CO colon  VS value start  VE value end (0 = empty)
- *   While header h is being parsed the capture pointer is cap0 + 16 + 8h and the
- *   no-event writes land in record h+1's LS slot (rewritten when h+1 starts),
- *   the terminal position in record h+1's CO slot.  VE slots must start at 0.
+ * Each event shifts its position into a 4-deep u16 history, which then holds
+ * everything a record needs (method start is 0: a leading empty line goes to
+ * the exact path).  The DFA only decides what it can decide without knowing
+ * where the buffer ends: a terminal is the reference's answer iff its byte
+ * lies before `len`; constructs that are rare or end-dependent go to the SLOW
+ * terminal and are re-parsed by the exact scalar path (rhp_scalar.h): leading
+ * CRLF, empty method, extra SP before the version, version other than
+ * HTTP/1.0 / HTTP/1.1, bare LF line ends, OWS before a CR (value trimming),
+ * obs-fold continuation lines, requests longer than kFastMaxLen.
  */
 #ifndef RHP_DFA_H
 #define RHP_DFA_H
 
 #include <stdint.h>
 
+#if defined(__HIPCC__)
+#define RHP_DHD __host__ __device__
+#else
+#define RHP_DHD
+#endif
+
 namespace rhp {
 
 enum State : uint32_t {
-  S_DONE = 0,     /* terminal: header section complete, TERM = position of final LF */
-  S_ERR1,         /* terminal: -1 decided at TERM (trusted iff TERM < len)          */
-  S_SLOW,         /* terminal: needs the exact scalar path                          */
-  S_OVF,          /* terminal: forced by the kernel when headers exceed capacity    */
-  S_SKIP3, S_SKIP2, S_SKIP1,   /* leading bytes of an unaligned 4-byte window   */
-  S_START, S_START_CR, S_METHOD0, S_METHOD, S_SPSKIP1, S_PATH, S_SPSKIP2,
-  S_V1, S_V2, S_V3, S_V4, S_V5, S_V6, S_V7, S_V8, S_CRLF_REQ,
-  S_LINE0, S_LINE, S_NAME, S_COLON, S_VALUE, S_VWS, S_VCR, S_END_CR0, S_END_CR,
+  /* plain rows (no event on entry) */
+  S_DONE = 0, S_ERR, S_SLOW,                   /* terminals */
+  S_SKIP3, S_SKIP2, S_SKIP1,                   /* leading bytes of an unaligned window */
+  S_METHOD0, S_METHOD, S_SP1, S_PATH,
+  S_V1, S_V2, S_V3, S_V4, S_V5, S_V6, S_V7, S_V8_0, S_V8_1, S_CRLF_RL,
+  S_LINE0, S_NAME, S_COLON, S_VALUE, S_VWS, S_VCR, S_END_CR,
+  S_NUM_PLAIN,
+  /* event rows (an event fires on the transition that enters them) */
+  S_DONE_E = S_NUM_PLAIN, S_ERR_E,             /* terminal events */
+  S_SP1_E,       /* ME */
+  S_PATH_E,      /* PS */
+  S_SP2_E,       /* PE */
+  S_CRLF_RL_E,   /* RL at the CR (HTTP/1.0) */
+  S_LINE0_E,     /* RL at the LF (HTTP/1.1) */
+  S_COLON_E,     /* CO */
+  S_VALUE_E,     /* VS */
+  S_VCR_E,       /* VS at the CR of an empty value */
+  S_LINE_E,      /* EOL */
   S_COUNT
 };
 
-/* capture slots, byte offsets from the capture pointer */
-enum Slot : uint32_t {
-  /* request-line phase (pointer = cap0) */
-  C_MS = 0, C_ME = 2, C_PS = 4, C_PE = 6, C_VD = 8, C_NONE_RL = 10, C_TERM_RL = 12,
-  /* header phase (pointer = record h) */
-  C_LS = 0, C_CO = 2, C_VS = 4, C_VE = 6, C_NONE_H = 8, C_TERM_H = 10,
-  /* terminal self-loops, either phase (record h+1's VE, or cap0+14) */
-  C_NONE_T = 14
-};
-
 enum : uint32_t {
-  kRowBytes = 1040,          /* 256 entries + 4 pad: rows rotate LDS banks by 4 */
-  kTableBytes = S_COUNT * kRowBytes,
-  kRlBytes = 16,             /* request-line record */
-  kHdrBytes = 8,             /* header record */
-  kInc0 = 16,                /* first header: cap0 -> record 0 */
-  kInc = 8
+  kRowBytes = 528,             /* 256 u16 entries + 16 pad: rows rotate LDS banks by 4 */
+  kEventBit = 14,
+  kEventRow = 1u << kEventBit, /* first event row */
+  kTableBytes = kEventRow + (S_COUNT - S_NUM_PLAIN) * kRowBytes,
+  kFastMaxLen = 65535 - 256    /* longer requests take the exact path (u16 positions) */
 };
+static_assert(S_NUM_PLAIN * kRowBytes <= kEventRow, "plain rows must fit below the event rows");
+static_assert(kTableBytes + 2 * 256 < 32768, "entries stay below bit 15");
 
-constexpr uint32_t row_of(uint32_t s) { return s * kRowBytes; }
-constexpr uint32_t entry(uint32_t next, uint32_t slot, uint32_t inc = 0)
+constexpr uint32_t row_of(uint32_t s)
 {
-  return row_of(next) | (slot << 16) | (inc << 24);
+  return s < S_NUM_PLAIN ? s * kRowBytes : kEventRow + (s - S_NUM_PLAIN) * kRowBytes;
 }
-constexpr uint32_t entry_next(uint32_t e) { return e & 0xffffu; }
-constexpr uint32_t entry_slot(uint32_t e) { return (e >> 16) & 0xffu; }
-constexpr uint32_t entry_inc(uint32_t e) { return e >> 24; }
-constexpr bool is_terminal_row(uint32_t row) { return row < row_of(S_SKIP3); }
+RHP_DHD constexpr bool is_terminal_row(uint32_t row)
+{
+  return row < row_of(S_SKIP3) || (row >= row_of(S_DONE_E) && row < row_of(S_SP1_E));
+}
+RHP_DHD constexpr bool is_done_row(uint32_t row) { return row == row_of(S_DONE) || row == row_of(S_DONE_E); }
+RHP_DHD constexpr bool is_err_row(uint32_t row) { return row == row_of(S_ERR) || row == row_of(S_ERR_E); }
+RHP_DHD constexpr uint32_t event_of(uint32_t row) { return row >> kEventBit; }
 
 constexpr bool c_tchar(uint32_t c)
 {
@@ -83,119 +98,152 @@ constexpr bool c_tchar(uint32_t c)
 constexpr bool c_ctl(uint32_t c) { return c < 0x20u || c == 0x7fu; }   /* CTL or DEL */
 constexpr bool c_ows(uint32_t c) { return c == ' ' || c == '\t'; }
 
-/* one transition: the reference's behaviour on byte c in state s */
+/* one transition: the next state on byte c in state s (picohttpparser.c line refs) */
 constexpr uint32_t step(uint32_t s, uint32_t c)
 {
   switch (s) {
-  case S_DONE: case S_ERR1: case S_SLOW: case S_OVF:
-    return entry(s, C_NONE_T);
-  case S_SKIP3: return entry(S_SKIP2, C_NONE_RL);
-  case S_SKIP2: return entry(S_SKIP1, C_NONE_RL);
-  case S_SKIP1: return entry(S_START, C_NONE_RL);
-  case S_START:     /* one optional leading CRLF / LF (picohttpparser.c:345-352) */
-    if (c == '\r') return entry(S_START_CR, C_NONE_RL);
-    if (c == '\n') return entry(S_METHOD0, C_NONE_RL);
-    return step(S_METHOD0, c);
-  case S_START_CR:
-    return c == '\n' ? entry(S_METHOD0, C_NONE_RL) : entry(S_ERR1, C_TERM_RL);
-  case S_METHOD0:   /* ADVANCE_TOKEN(method) first byte (:71-94,:355) */
-    if (c == ' ') return entry(S_SLOW, C_TERM_RL);          /* empty method */
-    if (c_ctl(c)) return entry(S_ERR1, C_TERM_RL);
-    return entry(S_METHOD, C_MS);
+  case S_DONE: case S_DONE_E: return S_DONE;
+  case S_ERR: case S_ERR_E: return S_ERR;
+  case S_SLOW: return S_SLOW;
+  case S_SKIP3: return S_SKIP2;
+  case S_SKIP2: return S_SKIP1;
+  case S_SKIP1: return S_METHOD0;
+  case S_METHOD0:   /* optional leading empty line (:345-352) -> exact path; ADVANCE_TOKEN (:71-94) */
+    if (c == '\r' || c == '\n' || c == ' ') return S_SLOW;
+    return c_ctl(c) ? S_ERR_E : S_METHOD;
   case S_METHOD:
-    if (c == ' ') return entry(S_SPSKIP1, C_ME);
-    if (c_ctl(c)) return entry(S_ERR1, C_TERM_RL);
-    return entry(S_METHOD, C_NONE_RL);
-  case S_SPSKIP1:   /* do ++buf while SP (:356-358), then path token (:359) */
-    if (c == ' ') return entry(S_SPSKIP1, C_NONE_RL);
-    if (c_ctl(c)) return entry(S_ERR1, C_TERM_RL);
-    return entry(S_PATH, C_PS);
-  case S_PATH:
-    if (c == ' ') return entry(S_SPSKIP2, C_PE);
-    if (c_ctl(c)) return entry(S_ERR1, C_TERM_RL);
-    return entry(S_PATH, C_NONE_RL);
-  case S_SPSKIP2:   /* SPs (:360-362), then "HTTP/1." + digit (:245-261) */
-    if (c == ' ') return entry(S_SPSKIP2, C_NONE_RL);
-    return c == 'H' ? entry(S_V1, C_NONE_RL) : entry(S_SLOW, C_TERM_RL);
-  case S_V1: return c == 'T' ? entry(S_V2, C_NONE_RL) : entry(S_SLOW, C_TERM_RL);
-  case S_V2: return c == 'T' ? entry(S_V3, C_NONE_RL) : entry(S_SLOW, C_TERM_RL);
-  case S_V3: return c == 'P' ? entry(S_V4, C_NONE_RL) : entry(S_SLOW, C_TERM_RL);
-  case S_V4: return c == '/' ? entry(S_V5, C_NONE_RL) : entry(S_SLOW, C_TERM_RL);
-  case S_V5: return c == '1' ? entry(S_V6, C_NONE_RL) : entry(S_SLOW, C_TERM_RL);
-  case S_V6: return c == '.' ? entry(S_V7, C_NONE_RL) : entry(S_SLOW, C_TERM_RL);
-  case S_V7: return (c >= '0' && c <= '9') ? entry(S_V8, C_VD) : entry(S_SLOW, C_TERM_RL);
-  case S_V8:        /* request line ends with CRLF or LF (:370-378) */
-    if (c == '\r') return entry(S_CRLF_REQ, C_NONE_RL);
-    if (c == '\n') return entry(S_LINE0, C_NONE_RL);
-    return entry(S_ERR1, C_TERM_RL);
-  case S_CRLF_REQ:
-    return c == '\n' ? entry(S_LINE0, C_NONE_RL) : entry(S_ERR1, C_TERM_RL);
-  case S_LINE0:     /* first header line (:266-311), obs-fold impossible */
-    if (c == '\r') return entry(S_END_CR0, C_NONE_RL);
-    if (c == '\n') return entry(S_DONE, C_TERM_RL);
-    if (c_tchar(c)) return entry(S_NAME, C_LS, kInc0);
-    return entry(S_ERR1, C_TERM_RL);
-  case S_LINE:
-    if (c == '\r') return entry(S_END_CR, C_NONE_H);
-    if (c == '\n') return entry(S_DONE, C_TERM_H);
-    if (c_tchar(c)) return entry(S_NAME, C_LS, kInc);
-    if (c_ows(c)) return entry(S_SLOW, C_TERM_H);           /* obs-fold */
-    return entry(S_ERR1, C_TERM_H);
+    if (c == ' ') return S_SP1_E;
+    return c_ctl(c) ? S_ERR_E : S_METHOD;
+  case S_SP1: case S_SP1_E:   /* do ++buf while SP (:356-358), then the path token (:359) */
+    if (c == ' ') return S_SP1;
+    return c_ctl(c) ? S_ERR_E : S_PATH_E;
+  case S_PATH: case S_PATH_E:
+    if (c == ' ') return S_SP2_E;
+    return c_ctl(c) ? S_ERR_E : S_PATH;
+  case S_SP2_E:     /* "HTTP/1." + digit (:245-261) right after one SP */
+    return c == 'H' ? S_V1 : S_SLOW;
+  case S_V1: return c == 'T' ? S_V2 : S_SLOW;
+  case S_V2: return c == 'T' ? S_V3 : S_SLOW;
+  case S_V3: return c == 'P' ? S_V4 : S_SLOW;
+  case S_V4: return c == '/' ? S_V5 : S_SLOW;
+  case S_V5: return c == '1' ? S_V6 : S_SLOW;
+  case S_V6: return c == '.' ? S_V7 : S_SLOW;
+  case S_V7: return c == '0' ? S_V8_0 : c == '1' ? S_V8_1 : S_SLOW;
+  case S_V8_0:      /* the request line ends with CRLF (:370-378); bare LF -> exact path */
+    if (c == '\r') return S_CRLF_RL_E;
+    return c == '\n' ? S_SLOW : S_ERR_E;
+  case S_V8_1:
+    if (c == '\r') return S_CRLF_RL;
+    return c == '\n' ? S_SLOW : S_ERR_E;
+  case S_CRLF_RL_E: return c == '\n' ? S_LINE0 : S_ERR_E;
+  case S_CRLF_RL: return c == '\n' ? S_LINE0_E : S_ERR_E;
+  case S_LINE0: case S_LINE0_E:   /* first header line (:266-311): no obs-fold yet */
+    if (c == '\r') return S_END_CR;
+    if (c == '\n') return S_SLOW;
+    return c_tchar(c) ? S_NAME : S_ERR_E;
+  case S_LINE_E:
+    if (c == '\r') return S_END_CR;
+    if (c == '\n' || c_ows(c)) return S_SLOW;   /* bare LF, obs-fold */
+    return c_tchar(c) ? S_NAME : S_ERR_E;
   case S_NAME:      /* name bytes must be tchar up to ':' (:297-310) */
-    if (c == ':') return entry(S_COLON, C_CO);
-    if (c_tchar(c)) return entry(S_NAME, C_NONE_H);
-    return entry(S_ERR1, C_TERM_H);
-  case S_COLON:     /* OWS after ':' (:312-317), then get_token_to_eol (:134-195) */
-    if (c_ows(c)) return entry(S_COLON, C_NONE_H);
-    if (c == '\r') return entry(S_VCR, C_VS);
-    if (c == '\n') return entry(S_LINE, C_VS);
-    if (c_ctl(c)) return entry(S_ERR1, C_TERM_H);
-    return entry(S_VALUE, C_VS);
-  case S_VALUE:     /* VE = start of the latest OWS run, or the EOL (:327-336) */
-    if (c_ows(c)) return entry(S_VWS, C_VE);
-    if (c == '\r') return entry(S_VCR, C_VE);
-    if (c == '\n') return entry(S_LINE, C_VE);
-    if (c_ctl(c)) return entry(S_ERR1, C_TERM_H);
-    return entry(S_VALUE, C_NONE_H);
-  case S_VWS:
-    if (c_ows(c)) return entry(S_VWS, C_NONE_H);
-    if (c == '\r') return entry(S_VCR, C_NONE_H);
-    if (c == '\n') return entry(S_LINE, C_NONE_H);
-    if (c_ctl(c)) return entry(S_ERR1, C_TERM_H);
-    return entry(S_VALUE, C_NONE_H);
-  case S_VCR:
-    return c == '\n' ? entry(S_LINE, C_NONE_H) : entry(S_ERR1, C_TERM_H);
-  case S_END_CR0:   /* empty line ends the headers (:268-275) */
-    return c == '\n' ? entry(S_DONE, C_TERM_RL) : entry(S_ERR1, C_TERM_RL);
-  case S_END_CR:
-    return c == '\n' ? entry(S_DONE, C_TERM_H) : entry(S_ERR1, C_TERM_H);
-  default:
-    return entry(S_SLOW, C_NONE_T);
+    if (c == ':') return S_COLON_E;
+    return c_tchar(c) ? S_NAME : S_ERR_E;
+  case S_COLON: case S_COLON_E:   /* OWS after ':' (:312-317), then get_token_to_eol (:134-195) */
+    if (c_ows(c)) return S_COLON;
+    if (c == '\r') return S_VCR_E;
+    if (c == '\n') return S_SLOW;
+    return c_ctl(c) ? S_ERR_E : S_VALUE_E;
+  case S_VALUE: case S_VALUE_E:
+    if (c_ows(c)) return S_VWS;
+    if (c == '\r') return S_VCR;
+    if (c == '\n') return S_SLOW;
+    return c_ctl(c) ? S_ERR_E : S_VALUE;
+  case S_VWS:       /* OWS inside a value; OWS before the EOL is trimmed (:327-336) -> exact */
+    if (c_ows(c)) return S_VWS;
+    if (c == '\r' || c == '\n') return S_SLOW;
+    return c_ctl(c) ? S_ERR_E : S_VALUE;
+  case S_VCR: case S_VCR_E: return c == '\n' ? S_LINE_E : S_ERR_E;
+  case S_END_CR:    /* empty line ends the headers (:268-275) */
+    return c == '\n' ? S_DONE_E : S_ERR_E;
+  default: return S_SLOW;
   }
 }
 
 struct Table {
-  uint32_t w[kTableBytes / 4];
+  uint16_t w[kTableBytes / 2];
 };
 
 constexpr Table make_table()
 {
   Table t{};
-  for (uint32_t s = 0; s < S_COUNT; s++) {
-    for (uint32_t c = 0; c < 256; c++) t.w[(row_of(s) >> 2) + c] = step(s, c);
-    for (uint32_t c = 256; c < kRowBytes / 4; c++) t.w[(row_of(s) >> 2) + c] = entry(S_SLOW, C_NONE_T);
-  }
+  for (uint32_t i = 0; i < kTableBytes / 2; i++) t.w[i] = (uint16_t) row_of(S_SLOW);
+  for (uint32_t s = 0; s < S_COUNT; s++)
+    for (uint32_t c = 0; c < 256; c++) t.w[(row_of(s) >> 1) + c] = (uint16_t) row_of(step(s, c));
   return t;
 }
 
-/* bytes of per-lane capture area for a header capacity; the kernel checks the
- * header count every kCheckSteps bytes, and a header line is >= 3 bytes, so at
- * most kCheckSteps/3 + 1 records can start past capacity before the check, plus
- * one for the next-record slots. */
-enum : uint32_t { kCheckSteps = 16 };
-constexpr uint32_t cap_bytes(uint32_t max_headers)
+/*
+ * Event decoder state of one request.  hist holds the last four event positions
+ * as u16: h01 = e0 | e1 << 16, h23 = e2 | e3 << 16 (e0 newest).
+ */
+struct Dec {
+  uint32_t h01, h23;
+  uint32_t k;       /* events consumed: 0..3 request line, then 4,5,6 = CO, VS, EOL */
+  uint32_t nh;      /* header lines completed */
+  uint32_t rl01;    /* method_len | path_off << 16 */
+  uint32_t rl23;    /* path_len | minor << 16 */
+  uint32_t ovf;     /* 0, or 1 + the position at which max_headers overflowed */
+};
+
+RHP_DHD inline void dec_reset(Dec &d)
 {
-  return kRlBytes + kHdrBytes * (max_headers + kCheckSteps / 3 + 3);
+  d.h01 = d.h23 = 0;
+  d.k = 0;
+  d.nh = 0;
+  d.rl01 = d.rl23 = 0;
+  d.ovf = 0;
+}
+
+/*
+ * Consume one (non-terminal) event at position p.  Returns true when a header
+ * record completed that is to be stored at index d.nh - 1 (< max_headers):
+ * (lo, hi) = (name_off | name_len << 16, value_off | value_len << 16).
+ * Sets d.ovf when the reference's max_headers check fires (picohttpparser.c:
+ * 281-284: a new line starts while num_headers == max_headers).
+ */
+RHP_DHD inline bool dec_event(Dec &d, uint32_t p, uint32_t maxh, uint32_t &lo, uint32_t &hi)
+{
+  d.h23 = (d.h23 << 16) | (d.h01 >> 16);
+  d.h01 = (d.h01 << 16) | p;
+  if (d.k < 3) {
+    d.k++;
+    return false;
+  }
+  if (d.k == 3) {   /* RL: history = RL, PE, PS, ME */
+    const uint32_t pe = d.h01 >> 16, ps = d.h23 & 0xffffu, me = d.h23 >> 16;
+    const uint32_t minor = p - pe - 9u;   /* 0 (event at the CR) or 1 (at the LF) */
+    d.rl01 = me | (ps << 16);
+    d.rl23 = (pe - ps) | (minor << 16);
+    d.h01 = (d.h01 & 0xffff0000u) | (pe + 10u);   /* e0 := the LF that ends the request line */
+    d.k = 4;
+    return false;
+  }
+  if (d.k == 4) {   /* CO: history = CO, prevLF, ... */
+    if (d.nh == maxh && d.ovf == 0) d.ovf = 1u + (d.h01 >> 16) + 1u;
+    d.k = 5;
+    return false;
+  }
+  if (d.k == 5) {   /* VS */
+    d.k = 6;
+    return false;
+  }
+  /* EOL: history = LF, VS, CO, prevLF */
+  const uint32_t lf = p, vs = d.h01 >> 16, co = d.h23 & 0xffffu, prev = d.h23 >> 16;
+  lo = (prev + 1u) | ((co - prev - 1u) << 16);
+  hi = vs | ((lf - 1u - vs) << 16);
+  d.k = 4;
+  d.nh++;
+  return d.nh <= maxh;
 }
 
 }  // namespace rhp

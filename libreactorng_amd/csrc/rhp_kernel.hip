@@ -5,16 +5,22 @@
  * http_read_request (http.c:177-234) over a batch of independent requests in
  * HBM.  Design:
  *
- *  - one request per lane, 64 requests per wave in flight, every lane runs the
- *    byte DFA of rhp_dfa.h in lockstep: per byte one LDS table read and one LDS
- *    u16 capture write, no divergence on the byte path;
- *  - each lane streams its own request through a 64-byte register window
- *    (4 x global_load_dwordx4), unaligned starts handled by SKIP states;
- *  - persistent waves pull chunks of requests from one atomic counter and hand
- *    requests to idle lanes at 64-byte block boundaries (ragged lengths);
- *  - a request whose outcome depends on where the buffer ends, or that takes a
- *    rare path (rhp_dfa.h S_SLOW), is finished by the exact scalar path
- *    (rhp_scalar.h) on the same lane.
+ *  - one request per lane, 64 requests per wave in flight; every lane runs the
+ *    byte DFA of rhp_dfa.h in lockstep: per byte one ds_read_u16 of the table in
+ *    LDS and two VALU ops that OR the entry's event bit into a 64-bit block
+ *    mask -- no LDS write and no divergence on the byte path;
+ *  - lanes stream their request in 64-byte windows (4 x global_load_dwordx4 at
+ *    4-byte alignment; unaligned starts enter through SKIP states), the next
+ *    window issued a whole block ahead; every lane also holds its NEXT
+ *    request's offsets, so a request switch never waits on a dependent load;
+ *  - once per block the event mask is decoded (rhp_dfa.h dec_event) into the
+ *    request-line record and header records, which are stored to HBM in
+ *    16-byte pairs; finished requests are finalized and new ones handed out
+ *    (persistent waves pull 256-request chunks from one atomic counter);
+ *  - a request whose outcome depends on where its buffer ends, or that takes a
+ *    rare path (S_SLOW), is finished by the exact scalar path (rhp_scalar.h).
+ *
+ * The algorithm is mirrored block for block by rhp_emu.cpp (CPU tests).
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -42,45 +48,40 @@ struct Params {
   uint32_t n;
   uint32_t max_headers;
   uint32_t mode;
-  uint32_t cap_lane;     /* capture bytes per lane (multiple of 16) */
+  uint32_t pad;
 };
 
-enum : uint32_t { kChunk = 256, kFastMaxLen = RHP_MAX_LEN - 256 };
+enum : uint32_t { kPoolChunk = 256, kBlock = 64, kLdsTable = (kTableBytes + 15u) & ~15u };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-#define RHP_LDS __attribute__((address_space(3)))
 
-/* LDS accessors on raw 32-bit LDS byte addresses */
-__device__ __forceinline__ uint32_t lds_load_u32(uint32_t addr)
-{
-  return *(const RHP_LDS uint32_t *) (size_t) addr;
-}
-__device__ __forceinline__ void lds_store_u16(uint32_t addr, uint32_t v)
-{
-  *(RHP_LDS uint16_t *) (size_t) addr = (uint16_t) v;
-}
-__device__ __forceinline__ uint32_t lds_load_u16(uint32_t addr)
-{
-  return *(const RHP_LDS uint16_t *) (size_t) addr;
-}
-__device__ __forceinline__ void lds_store_u32x4(uint32_t addr, u32x4 v)
-{
-  *(RHP_LDS u32x4 *) (size_t) addr = v;
-}
+#ifdef RHP_STAMPS
+/* diagnostic build only: per-wave cycle sums per loop section (never read by the kernel) */
+__device__ unsigned long long g_stamps[8192 * 8];
+#define RHP_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory"); \
+    __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define RHP_STAMP(t) do { } while (0)
+#endif
 
 /* 16 bytes at a 4-byte aligned global address */
-__device__ __forceinline__ u32x4 load_window16(const uint8_t *p)
+__device__ __forceinline__ u32x4 load_chunk(const uint8_t *p)
 {
   typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
   return *reinterpret_cast<const u32x4a4 *>(p);
 }
 
-/* ---- per-request completion ---- */
-
-/* Exact scalar path for one request (phr or http mode). */
-__device__ void finish_exact(const Params &p, uint32_t i, uint64_t off, uint64_t len)
+/* Exact scalar path for one request (phr or http mode).  Not inlined: it is the
+ * rare path, and keeping it out of the DFA loop keeps the loop's registers low. */
+__device__ __noinline__ void finish_exact(const Params &p, uint32_t i, uint64_t off, uint64_t len)
 {
+#ifdef RHP_EXPERIMENT_NO_EXACT
+  p.reqs[i].ret = -9;
+  return;
+#endif
   rhp_req_t r;
   r.flags = RHP_F_EXACT;
   rhp_hdr_t *h = p.hdrs + (uint64_t) i * p.max_headers;
@@ -105,92 +106,42 @@ __device__ void finish_exact(const Params &p, uint32_t i, uint64_t off, uint64_t
   p.reqs[i] = r;
 }
 
-/* Decode the lane's capture area into records (DFA decided ret > 0). */
-__device__ void finish_fast_ok(const Params &p, uint32_t i, uint64_t off, uint64_t len, uint32_t cap0,
-                               uint32_t count, int32_t ret)
+/* http_read_request framing of a request the DFA parsed (http mode only) */
+__device__ __noinline__ void finish_http(const Params &p, uint32_t i, uint64_t off, uint64_t len, rhp_req_t r)
 {
-  rhp_req_t r;
-  uint32_t ms = lds_load_u16(cap0 + C_MS), me = lds_load_u16(cap0 + C_ME);
-  uint32_t ps = lds_load_u16(cap0 + C_PS), pe = lds_load_u16(cap0 + C_PE);
-  uint32_t vd = lds_load_u16(cap0 + C_VD);
-  r.ret = ret;
-  r.method_off = (uint8_t) ms;
-  r.method_len = (uint16_t) (me - ms);
-  r.path_off = (uint16_t) ps;
-  r.path_len = (uint16_t) (pe - ps);
-  r.minor_version = (int8_t) (p.bytes[off + vd] - '0');
-  r.num_headers = (uint16_t) count;
-  r.flags = 0;
-  p.reqs[i] = r;
-  rhp_hdr_t *h = p.hdrs + (uint64_t) i * p.max_headers;
-  for (uint32_t k = 0; k < count; k++) {
-    uint32_t rec = cap0 + kRlBytes + kHdrBytes * k;
-    uint32_t ls = lds_load_u16(rec + C_LS), co = lds_load_u16(rec + C_CO);
-    uint32_t vs = lds_load_u16(rec + C_VS), ve = lds_load_u16(rec + C_VE);
-    rhp_hdr_t o;
-    o.name_off = (uint16_t) ls;
-    o.name_len = (uint16_t) (co - ls);
-    o.value_off = (uint16_t) vs;
-    o.value_len = (uint16_t) (ve > vs ? ve - vs : 0);
-    h[k] = o;
-  }
-  if (p.mode == RHP_MODE_HTTP)
-    http_frame(p.bytes_rw + off, len, r, h, &p.http[i]);
+  http_frame(p.bytes_rw + off, len, r, p.hdrs + (uint64_t) i * p.max_headers, &p.http[i]);
 }
 
-__device__ void finish_fast_bad(const Params &p, uint32_t i)
+/* a 16-byte header-record pair, or a single record, at 4-byte alignment */
+__device__ __forceinline__ void store_pair(rhp_hdr_t *dst, u32x4 v)
 {
-  rhp_req_t r;
-  r.ret = -1;
-  r.method_len = r.path_off = r.path_len = 0;
-  r.method_off = 0; r.minor_version = -1; r.num_headers = 0; r.flags = 0;
-  p.reqs[i] = r;
-  if (p.mode == RHP_MODE_HTTP) {
-    rhp_http_t x = {-1, 0, 0, 0};
-    p.http[i] = x;
-  }
+  typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+  *reinterpret_cast<u32x4a4 *>(dst) = v;
 }
-
-/*
- * Finalize the lane's request after the DFA stopped or ran past `len`.
- * Decision table (rhp_dfa.h header): a terminal decided at byte TERM is the
- * reference's answer iff TERM < len; anything else is re-parsed exactly.
- */
-__device__ void finalize(const Params &p, uint32_t i, uint64_t off, uint64_t len, uint32_t st,
-                         uint32_t cap0, uint32_t cap)
+__device__ __forceinline__ void store_one(rhp_hdr_t *dst, u32x2 v)
 {
-  uint32_t row = entry_next(st);
-  uint32_t count = cap == cap0 ? 0u : (cap - cap0 - kRlBytes) / kHdrBytes + 1u;
-  uint32_t term = lds_load_u16(cap == cap0 ? cap0 + C_TERM_RL : cap + C_TERM_H);
-  if (row == row_of(S_DONE) && term < len) {
-    if (count > p.max_headers) finish_fast_bad(p, i);
-    else finish_fast_ok(p, i, off, len, cap0, count, (int32_t) term + 1);
-  } else if ((row == row_of(S_ERR1) && term < len) || row == row_of(S_OVF)) {
-    finish_fast_bad(p, i);
-  } else {
-    finish_exact(p, i, off, len);
-  }
+  typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+  *reinterpret_cast<u32x2a4 *>(dst) = v;
 }
 
 }  // namespace
 
 /*
- * The DFA kernel.  One workgroup = WAVES waves; dynamic LDS = table + per-lane
- * capture areas.  Persistent: grid = workgroups resident on the device.
+ * The DFA kernel.  One workgroup = WAVES waves sharing one LDS copy of the
+ * table.  Persistent: grid = workgroups resident on the device.
  */
-template <int WAVES, int FLAGS>
+template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
 {
-  /* FLAGS bit 0: prefetch the next 64-byte window while the current one is parsed
-   * FLAGS bit 1: odd-dword capture stride (conflict-free LDS capture writes) */
-  constexpr bool kPrefetch = FLAGS & 1;
-  constexpr bool kOddStride = FLAGS & 2;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
+#ifdef RHP_STAMPS
   const uint32_t wave = tid >> 6;
+  unsigned long long t_entry = 0;
+  RHP_STAMP(t_entry);
+#endif
 
-  /* stage the transition table into LDS (it sits at LDS address 0) */
   {
     const u32x4 *src = reinterpret_cast<const u32x4 *>(&g_table);
     u32x4 *dst = reinterpret_cast<u32x4 *>(lds);
@@ -198,107 +149,240 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
   }
   __syncthreads();
 
-  const uint32_t lds_base = (uint32_t) (size_t) (RHP_LDS uint8_t *) lds;   /* LDS address of lds[0] */
-  const uint32_t cap0 = lds_base + kTableBytes + (wave * 64u + lane) * p.cap_lane;
-  /* capture pointer value once max_headers records have started */
-  const uint32_t cap_limit = p.max_headers ? cap0 + kRlBytes + kHdrBytes * (p.max_headers - 1) : cap0;
+  const uint32_t maxh = p.max_headers;
+  const uint32_t park = row_of(S_DONE);
 
-  /* lane state */
-  uint32_t st = entry(S_DONE, C_NONE_T);
-  uint32_t cap = cap0;
-  int32_t pos = 0;
-  bool has = false;
-  uint32_t req = 0;
-  uint64_t off = 0, len = 0;
-  const uint8_t *win = p.bytes;
+  /* ---- lane state ---- */
+  uint32_t st = park;                  /* LDS offset of the current state's row (= the last entry) */
+  int32_t pos = 0, block_pos = 0;      /* request-relative position of the next byte / of the block */
+  uint32_t ev_lo = 0, ev_hi = 0;       /* events of the block just stepped */
+  bool has = false;                    /* cur is being parsed */
+  uint32_t cur = 0, cur_len = 0;
+  uint64_t cur_off = 0, cur_ptr = 0;   /* cur_ptr: byte offset of the window in W */
+  Dec d;
+  dec_reset(d);
+  uint32_t rec_lo = 0, rec_hi = 0;     /* header record waiting for its pair */
+  bool pend_ok = false;                /* pend: the lane's next request */
+  uint32_t pend = 0;
+  uint64_t pend_o0 = 0, pend_o1 = 0;   /* offsets[pend], offsets[pend+1] as loaded */
+  uint32_t nw_kind = 0;                /* next window: 0 none, 1 continuation, 2 first window of pend */
+  uint64_t nw_ptr = 0;
+  u32x4 W[4], NW[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) W[q] = NW[q] = u32x4{0, 0, 0, 0};
 
-  bool fresh = false;                 /* lane got a new request at this boundary */
-  u32x4 wn[4] = {u32x4{0, 0, 0, 0}, u32x4{0, 0, 0, 0}, u32x4{0, 0, 0, 0}, u32x4{0, 0, 0, 0}};
-
-  /* wave-uniform pool of requests */
+  /* ---- wave-uniform request pool ----
+   * Requests are handed out in chunks of kPoolChunk.  Wave g of the grid owns
+   * chunk g outright; chunks past the grid's first round come from one atomic
+   * counter (only touched when the batch has more chunks than waves), so the
+   * launch does not start with every wave contending for one address. */
+  const uint32_t nwaves = gridDim.x * WAVES;
+  const uint32_t nchunks = (p.n + kPoolChunk - 1) / kPoolChunk;
   uint32_t pool_next = 0, pool_end = 0;
+  uint32_t next_chunk = blockIdx.x * WAVES + (tid >> 6);   /* wave-uniform */
   bool pool_dry = false;
 
-  for (;;) {
-    /* ---- block boundary: finish lanes that are done or past their end ---- */
-    if (has) {
-      bool term = is_terminal_row(entry_next(st));
-      if (term || pos >= (int32_t) len) {
-        finalize(p, req, off, len, st, cap0, cap);
-        has = false;
-      }
-    }
-    /* ---- hand requests to idle lanes ---- */
-    uint64_t idle = __ballot(!has);
-    while (idle && !pool_dry) {
+  /* give every lane without a pending request one from the pool; the offsets
+   * loads are only consumed at the top of the next block */
+  auto refill_pend = [&]() {
+    uint64_t want = __ballot(!pend_ok);
+    while (want && !pool_dry) {
       if (pool_next >= pool_end) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&p.work[0], (uint32_t) kChunk);
-        base = __builtin_amdgcn_readfirstlane(base);
-        if (base >= p.n) { pool_dry = true; break; }
-        pool_next = base;
-        pool_end = min(base + (uint32_t) kChunk, p.n);
-      }
-      uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) idle, 0));
-      uint32_t avail = pool_end - pool_next;
-      if (!has && rank < avail) {
-        req = pool_next + rank;
-        off = p.offsets[req];
-        len = p.offsets[req + 1] - off;
-        has = true;
-        uint32_t mis = (uint32_t) off & 3u;
-        win = p.bytes + (off - mis);
-        pos = -(int32_t) mis;
-        uint32_t s0 = mis == 0 ? S_START : mis == 1 ? S_SKIP1 : mis == 2 ? S_SKIP2 : S_SKIP3;
-        if (len > kFastMaxLen) s0 = S_SLOW;
-        st = entry(s0, C_NONE_RL);
-        cap = cap0;
-        if (kOddStride) {
-          /* only the VE slots must start at 0 (rhp_dfa.h) */
-          for (uint32_t b = kRlBytes + C_VE; b + 2 <= p.cap_lane; b += kHdrBytes) lds_store_u16(cap0 + b, 0);
-        } else {
-          for (uint32_t b = 0; b < p.cap_lane; b += 16) lds_store_u32x4(cap0 + b, u32x4{0, 0, 0, 0});
+        uint32_t c = next_chunk;
+        if (c == 0xffffffffu) {
+          if (nchunks <= nwaves) { pool_dry = true; break; }
+          uint32_t k = 0;
+          if (lane == 0) k = atomicAdd(&p.work[0], 1u);
+          c = nwaves + __builtin_amdgcn_readfirstlane(k);
         }
-        fresh = true;
+        next_chunk = 0xffffffffu;
+        if (c >= nchunks) { pool_dry = true; break; }
+        pool_next = c * kPoolChunk;
+        pool_end = min(pool_next + (uint32_t) kPoolChunk, p.n);
       }
-      uint32_t k = (uint32_t) __popcll(idle);
-      pool_next += min(k, avail);
-      idle = __ballot(!has);
+      uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
+      uint32_t avail = pool_end - pool_next;
+      if (!pend_ok && rank < avail) {
+        pend = pool_next + rank;
+        pend_o0 = p.offsets[pend];
+        pend_o1 = p.offsets[pend + 1];
+        pend_ok = true;
+      }
+      pool_next += min((uint32_t) __popcll(want), avail);
+      want = __ballot(!pend_ok);
     }
-    if (!__ballot(has)) break;
+  };
 
-    /* ---- one 64-byte block: 4 sub-blocks of 16 steps ---- */
-    u32x4 w[4];
-    if (kPrefetch) {
-#pragma unroll
-      for (int q = 0; q < 4; q++) w[q] = fresh ? load_window16(win + 16 * q) : wn[q];
-#pragma unroll
-      for (int q = 0; q < 4; q++) wn[q] = has ? load_window16(win + 64 + 16 * q) : u32x4{0, 0, 0, 0};
+  /*
+   * Decode the block's events and finalize cur when its outcome is known
+   * (decisions mirrored by rhp_emu.cpp):
+   *   ok    DONE at term < len
+   *   bad   ERR at term < len, or max_headers overflow at a line start < len
+   *   exact SLOW, a terminal at/after len, or no terminal by the end of the buffer
+   */
+  auto decode = [&]() {
+    if (!has) return;
+    const uint32_t row = st;
+    const bool slow = row == row_of(S_SLOW);
+    const bool term_ev = is_done_row(row) || is_err_row(row);   /* its last event is the terminal */
+    uint32_t mlo = slow ? 0u : ev_lo, mhi = slow ? 0u : ev_hi;
+    uint32_t term_pos = 0xffffffffu;
+    rhp_hdr_t *hout = p.hdrs + (uint64_t) cur * maxh;
+    while (__ballot((mlo | mhi) != 0)) {
+      if ((mlo | mhi) != 0) {
+        uint32_t b;
+        if (mlo) { b = __builtin_ctz(mlo); mlo &= mlo - 1u; }
+        else { b = 32u + __builtin_ctz(mhi); mhi &= mhi - 1u; }
+        const uint32_t ep = (uint32_t) (block_pos + (int32_t) b);
+        if (term_ev && (mlo | mhi) == 0) {
+          term_pos = ep;
+        } else {
+          uint32_t lo, hi;
+          if (dec_event(d, ep, maxh, lo, hi)) {
+            if (d.nh & 1u) { rec_lo = lo; rec_hi = hi; }
+            else if (!(p.pad & 2)) store_pair(hout + d.nh - 2u, u32x4{rec_lo, rec_hi, lo, hi});
+          }
+          if (d.ovf) { mlo = mhi = 0; }
+        }
+      }
+    }
+    const bool ovf = d.ovf != 0;
+    const bool fin = ovf || slow || term_ev || pos >= (int32_t) cur_len;
+    if (!fin) return;
+    const bool ok = !ovf && is_done_row(row) && term_pos < cur_len;
+    const bool bad = ovf ? d.ovf - 1u < cur_len : (is_err_row(row) && term_pos < cur_len);
+    if (ok) {
+      if ((d.nh & 1u) && !(p.pad & 2)) store_one(hout + d.nh - 1u, u32x2{rec_lo, rec_hi});
+      rhp_req_t r;
+      r.ret = (int32_t) term_pos + 1;
+      r.method_len = (uint16_t) d.rl01;
+      r.path_off = (uint16_t) (d.rl01 >> 16);
+      r.path_len = (uint16_t) d.rl23;
+      r.method_off = 0;
+      r.minor_version = (int8_t) (d.rl23 >> 16);
+      r.num_headers = (uint16_t) d.nh;
+      r.flags = 0;
+      if (!(p.pad & 2)) p.reqs[cur] = r;
+      if (p.mode == RHP_MODE_HTTP) finish_http(p, cur, cur_off, cur_len, r);
+    } else if (bad) {
+      rhp_req_t r;
+      r.ret = -1;
+      r.method_len = r.path_off = r.path_len = 0;
+      r.method_off = 0; r.minor_version = -1; r.num_headers = 0; r.flags = 0;
+      p.reqs[cur] = r;
+      if (p.mode == RHP_MODE_HTTP) {
+        rhp_http_t x = {-1, 0, 0, 0};
+        p.http[cur] = x;
+      }
     } else {
-#pragma unroll
-      for (int q = 0; q < 4; q++) w[q] = has ? load_window16(win + 16 * q) : u32x4{0, 0, 0, 0};
+      finish_exact(p, cur, cur_off, cur_len);
     }
-    fresh = false;
+    has = false;
+    st = park;
+  };
 
+  /* 16 DFA steps over one 16-byte chunk; events -> bits [base, base+16) of ev */
+  auto steps = [&](const u32x4 &chunk, uint32_t &ev, const int base) {
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-#pragma unroll
-      for (int k = 0; k < 16; k++) {
-        uint32_t c = (w[q][k >> 2] >> ((k & 3) * 8)) & 0xffu;
-        uint32_t e = lds_load_u32(lds_base + entry_next(st) + c * 4u);
-        cap += entry_inc(e);
-        lds_store_u16(cap + entry_slot(e), (uint32_t) pos);
-        pos++;
-        st = e;
-      }
-      /* header records beyond capacity: stop the lane (rhp_dfa.h cap_bytes) */
-      if (__ballot(cap > cap_limit && !is_terminal_row(entry_next(st)))) {
-        if (cap > cap_limit && !is_terminal_row(entry_next(st)))
-          st = entry(pos <= (int32_t) len ? S_OVF : S_SLOW, C_NONE_T);
-      }
+    for (int k = 0; k < 16; k++) {
+      const uint32_t c = (chunk[k >> 2] >> ((k & 3) * 8)) & 0xffu;
+      st = *reinterpret_cast<const uint16_t *>(lds + st + c * 2u);
+      ev |= (st >> kEventBit) << (base + k);
     }
-    win += 64;
+  };
+
+  refill_pend();
+
+#ifdef RHP_STAMPS
+  unsigned long long t0 = 0, t1 = 0, acc[6] = {0, 0, 0, 0, 0, 0}, t_loop = 0;
+  RHP_STAMP(t_loop);
+#endif
+  /*
+   * One iteration = one 64-byte window per lane.
+   * [A] take the loads issued one block earlier (window, pending offsets): the
+   * loop's only VMEM wait -> [B] decode + finalize the previous block (its
+   * stores are older than any load the next [A] waits for) -> [C] switch to the
+   * landed window -> [D] hand out pending requests -> [E] issue the next
+   * window's loads -> 64 DFA steps.
+   */
+  for (;;) {
+    RHP_STAMP(t0);
+    /* [A] */
+    const uint64_t p_o0 = pend_o0, p_o1 = pend_o1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) W[q] = NW[q];
+#ifdef RHP_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    RHP_STAMP(t1); acc[0] += t1 - t0; t0 = t1;
+#endif
+    /* [B] */
+    decode();
+#ifdef RHP_STAMPS
+    RHP_STAMP(t1); acc[1] += t1 - t0; t0 = t1;
+#endif
+    /* [C] */
+    if (nw_kind == 2) {
+      cur = pend; cur_off = p_o0; cur_len = (uint32_t) min(p_o1 - p_o0, (uint64_t) 0xffffffffu);
+      pend_ok = false;
+      has = true;
+      const uint32_t mis = (uint32_t) cur_off & 3u;
+      uint32_t s0 = mis == 0 ? S_METHOD0 : mis == 1 ? S_SKIP1 : mis == 2 ? S_SKIP2 : S_SKIP3;
+      if (cur_len > kFastMaxLen) s0 = S_SLOW;
+      st = row_of(s0);
+      pos = -(int32_t) mis;
+      dec_reset(d);
+    }
+    if (nw_kind) cur_ptr = nw_ptr;
+    const bool pend_ready = pend_ok;   /* assigned before this block: p_o0/p_o1 valid */
+    /* [D] */
+    refill_pend();
+#ifdef RHP_STAMPS
+    RHP_STAMP(t1); acc[2] += t1 - t0; t0 = t1;
+#endif
+    /* [E] next window: continuation of cur, else the first window of a ready pend */
+    nw_kind = 0;
+    if (has && cur_ptr + kBlock < cur_off + cur_len) {
+      nw_ptr = cur_ptr + kBlock;
+      nw_kind = 1;
+    } else if (pend_ready) {
+      nw_ptr = p_o0 & ~(uint64_t) 3;
+      nw_kind = 2;
+    }
+    {
+      /* p.pad bit 0 (experiment): read every window from the first 256 B of the
+       * batch (cache-resident) instead of the lane's own request */
+      const uint64_t src = (p.pad & 1) ? (nw_ptr & 192) : nw_ptr;
+#pragma unroll
+      for (int q = 0; q < 4; q++) NW[q] = nw_kind ? load_chunk(p.bytes + src + 16 * q) : u32x4{0, 0, 0, 0};
+    }
+    if (!__ballot(has || nw_kind || pend_ok)) break;
+#ifdef RHP_STAMPS
+    RHP_STAMP(t1); acc[3] += t1 - t0; t0 = t1;
+#endif
+    /* 64 steps (idle lanes step in the parked terminal state) */
+    block_pos = pos;
+    ev_lo = 0;
+    ev_hi = 0;
+    steps(W[0], ev_lo, 0);
+    steps(W[1], ev_lo, 16);
+    steps(W[2], ev_hi, 0);
+    steps(W[3], ev_hi, 16);
+    pos += (int32_t) kBlock;
+#ifdef RHP_STAMPS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    RHP_STAMP(t1); acc[4] += t1 - t0; acc[5] += 1;
+#endif
   }
+#ifdef RHP_STAMPS
+  if (lane == 0) {
+    const uint32_t w = (blockIdx.x * WAVES + wave) % 8192;
+    for (int k = 0; k < 6; k++) g_stamps[w * 8 + k] = acc[k];
+    unsigned long long t_exit = 0;
+    RHP_STAMP(t_exit);
+    g_stamps[w * 8 + 6] = t_loop - t_entry;
+    g_stamps[w * 8 + 7] = t_exit - t_entry;
+  }
+#endif
 
   /* the last workgroup out re-arms the work counters for the next launch, so a
    * step is exactly one kernel launch (no memset) */
@@ -327,54 +411,52 @@ __global__ __launch_bounds__(256) void rhp_exact_kernel(Params p)
 namespace {
 int g_impl = RHP_IMPL_DFA;
 int g_cus = 0;
-int g_flags = -1;   /* RHP_DFA_FLAGS (experiments); default below */
 
-int dfa_flags()
+template <int WAVES>
+int launch_dfa(const Params &prm, hipStream_t s)
 {
-  if (g_flags < 0) {
-    const char *e = getenv("RHP_DFA_FLAGS");
-    g_flags = e ? (atoi(e) & 3) : 3;
-  }
-  return g_flags;
-}
-
-template <int FLAGS>
-int launch_waves(int waves, const Params &prm, size_t lds, hipStream_t s)
-{
-  switch (waves) {
-  case 8: return launch_dfa<8, FLAGS>(prm, lds, s);
-  case 4: return launch_dfa<4, FLAGS>(prm, lds, s);
-  case 2: return launch_dfa<2, FLAGS>(prm, lds, s);
-  default: return launch_dfa<1, FLAGS>(prm, lds, s);
-  }
-}
-
-template <int WAVES, int FLAGS>
-int launch_dfa(const Params &prm, size_t lds_bytes, hipStream_t s)
-{
+  const size_t lds_bytes = kLdsTable;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES, FLAGS>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds_bytes);
     if (e != hipSuccess) return (int) e;
     attr_set = true;
   }
   int per_cu = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rhp_dfa_kernel<WAVES, FLAGS>, WAVES * 64,
-                                                               lds_bytes);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rhp_dfa_kernel<WAVES>, WAVES * 64, lds_bytes);
   if (e != hipSuccess) return (int) e;
   if (per_cu < 1) per_cu = 1;
   uint32_t grid = (uint32_t) (g_cus * per_cu);
   uint32_t need = (prm.n + 64 * WAVES - 1) / (64 * WAVES);
   if (grid > need) grid = need > 0 ? need : 1;
-  hipLaunchKernelGGL((rhp_dfa_kernel<WAVES, FLAGS>), dim3(grid), dim3(WAVES * 64), lds_bytes, s, prm);
+  hipLaunchKernelGGL(rhp_dfa_kernel<WAVES>, dim3(grid), dim3(WAVES * 64), lds_bytes, s, prm);
   return (int) hipGetLastError();
+}
+
+int g_waves = -1;   /* RHP_WAVES (experiments): waves per workgroup */
+
+int dfa_waves()
+{
+  if (g_waves < 0) {
+    const char *e = getenv("RHP_WAVES");
+    g_waves = e ? atoi(e) : 16;
+  }
+  return g_waves;
 }
 }  // namespace
 
 extern "C" {
 
-const char *rhp_version(void) { return "rhp 0.1.0 (gfx950)"; }
+const char *rhp_version(void) { return "rhp 0.3.0 (gfx950)"; }
+
+#ifdef RHP_STAMPS
+/* diagnostic build only: copy the per-wave section cycle sums (8192 x 8 u64) */
+int rhp_debug_stamps(unsigned long long *host)
+{
+  return (int) hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(g_stamps), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 const char *rhp_kernel_name(void) { return g_impl == RHP_IMPL_EXACT ? "rhp_exact_kernel" : "rhp_dfa_kernel"; }
 
@@ -401,6 +483,7 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
     if (e == hipSuccess) e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return (int) e;
   }
+
   Params prm;
   prm.bytes = b->bytes;
   prm.bytes_rw = b->bytes_rw;
@@ -412,9 +495,10 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.n = b->n;
   prm.max_headers = b->max_headers;
   prm.mode = b->mode;
-  const int flags = dfa_flags();
-  prm.cap_lane = (cap_bytes(b->max_headers) + 15u) & ~15u;
-  if (flags & 2) prm.cap_lane += 4;      /* odd number of dwords: lanes hit distinct banks */
+  {
+    const char *e = getenv("RHP_EXPERIMENT");   /* timing experiments only: breaks results */
+    prm.pad = e ? (uint32_t) atoi(e) : 0u;
+  }
 
   if (g_impl == RHP_IMPL_EXACT) {
     uint32_t grid = (b->n + 255) / 256;
@@ -422,19 +506,12 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
     hipLaunchKernelGGL(rhp_exact_kernel, dim3(grid), dim3(256), 0, s, prm);
     return (int) hipGetLastError();
   }
-  const size_t budget = 160 * 1024;
-  size_t per_wave = 64 * (size_t) prm.cap_lane;
-  for (int waves = 8; waves >= 1; waves >>= 1) {
-    size_t lds = kTableBytes + waves * per_wave;
-    if (lds > budget) continue;
-    switch (flags) {
-    case 0: return launch_waves<0>(waves, prm, lds, s);
-    case 1: return launch_waves<1>(waves, prm, lds, s);
-    case 2: return launch_waves<2>(waves, prm, lds, s);
-    default: return launch_waves<3>(waves, prm, lds, s);
-    }
+  switch (dfa_waves()) {
+  case 4: return launch_dfa<4>(prm, s);
+  case 8: return launch_dfa<8>(prm, s);
+  case 11: return launch_dfa<11>(prm, s);
+  default: return launch_dfa<16>(prm, s);
   }
-  return -12;
 }
 
 }  // extern "C"

@@ -140,3 +140,28 @@ def test_toolong_request_reported():
     buf, off = pack([b"GET / HTTP/1.1\r\n\r\n", big])
     res, _ = rhp.emulate(buf, off, 16)
     assert res.reqs["ret"][0] == 18 and res.reqs["ret"][1] == rhp.RHP_RET_TOOLONG
+
+
+def dense_header_batch(n=3000, seed=5):
+    """Adversarial: many 3-byte header lines ("a:\n") so up to 6 header records
+    start inside one 16-byte check interval (capture-ring wrap, request-line
+    clobber rule, flush ordering; rhp_dfa.h)."""
+    rng = np.random.default_rng(seed)
+    reqs = []
+    for _ in range(n):
+        rl = (b"GET /" + b"p" * int(rng.integers(0, 40)) + b" HTTP/1." + bytes([48 + int(rng.integers(0, 10))]) +
+              (b"\r\n" if rng.random() < .5 else b"\n"))
+        hs = b"".join((b"a:\n" if rng.random() < .6 else b"bb: v \r\n" if rng.random() < .5 else b"c:\r\n")
+                      for _ in range(int(rng.integers(0, 40))))
+        reqs.append(rl + hs + (b"\r\n" if rng.random() < .9 else b""))
+    return reqs
+
+
+@pytest.mark.parametrize("shift", [0, 3])
+def test_dense_headers_emulation(shift):
+    buf, off = pack(dense_header_batch(), align_shift=shift)
+    for maxh in (0, 6, 7, 8, 16, 64):
+        for mode in (rhp.MODE_PHR, rhp.MODE_HTTP):
+            res, _ = rhp.emulate(buf, off, maxh, mode)
+            want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
+            assert_same(canon(res, mode), want, buf, off, f"dense shift{shift} maxh{maxh} mode{mode}")

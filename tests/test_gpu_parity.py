@@ -10,7 +10,7 @@ import pytest
 
 import libreactorng_amd as rhp
 from oracle_util import assert_same, canon, run_oracle, to_rhp
-from test_cpu_units import EDGE, pack
+from test_cpu_units import EDGE, dense_header_batch, pack
 
 pytestmark = pytest.mark.gpu
 
@@ -54,8 +54,10 @@ def test_gpu_fuzz_vs_oracle(maxh):
         res = rhp.parse_batch(buf, off, maxh, mode)
         want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
         assert_same(canon(res, mode), want, buf, off, f"GPU fuzz cfg{cfg} maxh{maxh}")
-        # the DFA must decide most requests itself (the exact path is the rare path)
-        assert (res.reqs["flags"] & rhp.F_EXACT).mean() < 0.35
+        # the kernel takes the exact path for exactly the requests the emulator of
+        # its algorithm (rhp_emu.cpp) sends there
+        emu, _ = rhp.emulate(buf, off, maxh, mode)
+        assert np.array_equal(res.reqs["flags"] & rhp.F_EXACT, emu.reqs["flags"] & rhp.F_EXACT)
 
 
 @pytest.mark.parametrize("shift", [0, 1, 2, 3])
@@ -120,3 +122,13 @@ def test_gpu_full_size_configs_vs_oracle(cfg, maxh, mode):
     res = rhp.parse_batch(buf, off, maxh, mode)
     want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
     assert_same(canon(res, mode), want, buf, off, f"full size cfg{cfg} maxh{maxh}")
+
+
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+def test_gpu_dense_headers(shift):
+    buf, off = pack(dense_header_batch(4000, 11 + shift), align_shift=shift)
+    for maxh in (0, 6, 7, 8, 16, 64):
+        for mode in (rhp.MODE_PHR, rhp.MODE_HTTP):
+            res = rhp.parse_batch(buf, off, maxh, mode)
+            want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
+            assert_same(canon(res, mode), want, buf, off, f"GPU dense shift{shift} maxh{maxh} mode{mode}")

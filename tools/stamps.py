@@ -1,0 +1,43 @@
+"""Diagnostic: per-section cycle breakdown of rhp_dfa_kernel (RHP_STAMPS build).
+
+usage: python tools/stamps.py [config]   (needs libreactorng_amd/librhp_stamps.so)
+Also reports the wall span of the launch in s_memtime ticks against the HIP-event
+time of the same launch, i.e. the shader clock the kernel actually ran at.
+"""
+import ctypes, os, sys
+import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["RHP_LIB"] = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libreactorng_amd", "librhp_stamps.so")
+import torch
+import libreactorng_amd as rhp
+cfg = int(sys.argv[1]) if len(sys.argv) > 1 else rhp.GEN_GET256
+maxh = {rhp.GEN_ZIPF: 32}.get(cfg, 16)
+mode = rhp.MODE_HTTP if cfg == rhp.GEN_POST1K else rhp.MODE_PHR
+n = 1 << 20
+buf, off = rhp.generate(cfg, n, 0x5EED0002)
+db = rhp.DeviceBatch(buf, off, maxh, mode)
+for _ in range(3):
+    db.launch()
+torch.cuda.synchronize()
+a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+a.record()
+db.launch()
+b.record()
+torch.cuda.synchronize()
+ms = a.elapsed_time(b)
+st = np.zeros(8192 * 8, dtype=np.uint64)
+lib = rhp.lib()
+lib.rhp_debug_stamps.argtypes = [ctypes.c_void_p]
+assert lib.rhp_debug_stamps(st.ctypes.data) == 0
+st = st.reshape(8192, 8)
+used = st[:, 5] > 0
+f = st.astype(np.float64)
+tot = f[used, :5].sum(axis=0)
+names = ["A top wait", "B decode+finalize", "C+D switch/refill", "E window issue", "F 64 steps"]
+iters = f[used, 5].sum()
+print(f"config {cfg}: waves {used.sum()}  iterations {iters:.0f}  cycles/iteration per wave:")
+for k in range(5):
+    print(f"  {names[k]:22s} {tot[k] / iters:9.1f}  ({100 * tot[k] / tot.sum():.1f}%)")
+pre, whole = f[used, 6], f[used, 7]
+print(f"  launch {ms * 1e3:.1f} us (HIP events); per wave: entry->loop {pre.mean():.0f}, entry->exit mean {whole.mean():.0f}"
+      f" max {whole.max():.0f}, loop sections {tot.sum() / used.sum():.0f} (memtime ticks)")

@@ -49,9 +49,30 @@ struct Params {
   uint32_t max_headers;
   uint32_t mode;
   uint32_t pad;
+  uint32_t chunk;   /* requests per pool chunk (host: >= 256, sized so no wave needs > kChunkCap) */
 };
 
-enum : uint32_t { kPoolChunk = 256, kBlock = 64, kLdsTable = (kTableBytes + 15u) & ~15u };
+enum : uint32_t {
+  kPoolChunk = 256,
+  kBlock = 64,
+  kLdsTable = (kTableBytes + 1023u) & ~1023u,   /* staging starts 1 KiB aligned */
+  kStageBuf = 64 * kBlock,                       /* one window per lane */
+  kStageWave = 2 * kStageBuf,                    /* double-buffered */
+  kChunkCap = 32,                                /* chunks one wave may take (its replay list) */
+  kDeferExact = 0x8000u,                         /* reqs[i].flags while deferred (kernel-internal) */
+  kDeferFrame = 0x4000u
+};
+
+/* LDS byte address of part q (16 B) of lane w's window inside one staging
+ * buffer.  The LDS-DMA loads of a wave write lane-linearly (1 KiB per
+ * instruction), so the swizzle lives on the source side: instruction i, lane j
+ * fetches part ((j & 3) - (j >> 4)) & 3 of lane 16i + (j >> 2)'s window, which
+ * makes each lane's four ds_read_b128 of its own window bank-conflict free. */
+__device__ __forceinline__ uint32_t stage_off(uint32_t w, uint32_t q)
+{
+  const uint32_t u = w & 15u;
+  return (w >> 4) * 1024u + u * 64u + ((q + (u >> 2)) & 3u) * 16u;
+}
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -112,16 +133,36 @@ __device__ __noinline__ void finish_http(const Params &p, uint32_t i, uint64_t o
   http_frame(p.bytes_rw + off, len, r, p.hdrs + (uint64_t) i * p.max_headers, &p.http[i]);
 }
 
+/* Params pointers are generic in the kernel's view (they sit in a struct);
+ * the hot stores go through explicit global-address-space pointers so they are
+ * global_store (VM counter only), not flat_store (VM + LGKM). */
+#define GLOBAL(T, x) ((__attribute__((address_space(1))) T *) (x))
+
 /* a 16-byte header-record pair, or a single record, at 4-byte alignment */
 __device__ __forceinline__ void store_pair(rhp_hdr_t *dst, u32x4 v)
 {
   typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-  *reinterpret_cast<u32x4a4 *>(dst) = v;
+  *GLOBAL(u32x4a4, dst) = v;
 }
 __device__ __forceinline__ void store_one(rhp_hdr_t *dst, u32x2 v)
 {
   typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
-  *reinterpret_cast<u32x2a4 *>(dst) = v;
+  *GLOBAL(u32x2a4, dst) = v;
+}
+__device__ __forceinline__ void store_req(rhp_req_t *dst, const rhp_req_t &r)
+{
+  u32x4 v;
+  __builtin_memcpy(&v, &r, sizeof r);
+  *GLOBAL(u32x4, dst) = v;
+}
+__device__ __forceinline__ void store_http_bad(rhp_http_t *dst)
+{
+  /* {result -1, body_kind 0, consumed 0, body_len 0} */
+  typedef uint32_t u32x2a8 __attribute__((ext_vector_type(2), aligned(8)));
+  __attribute__((address_space(1))) u32x2a8 *q = GLOBAL(u32x2a8, dst);
+  q[0] = u32x2a8{0xffffffffu, 0u};
+  q[1] = u32x2a8{0u, 0u};
+  q[2] = u32x2a8{0u, 0u};
 }
 
 }  // namespace
@@ -167,9 +208,11 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
   uint64_t pend_o0 = 0, pend_o1 = 0;   /* offsets[pend], offsets[pend+1] as loaded */
   uint32_t nw_kind = 0;                /* next window: 0 none, 1 continuation, 2 first window of pend */
   uint64_t nw_ptr = 0;
-  u32x4 W[4], NW[4];
+  u32x4 W[4];
 #pragma unroll
-  for (int q = 0; q < 4; q++) W[q] = NW[q] = u32x4{0, 0, 0, 0};
+  for (int q = 0; q < 4; q++) W[q] = u32x4{0, 0, 0, 0};
+  const uint32_t stage = kLdsTable + (tid >> 6) * kStageWave;   /* this wave's two buffers */
+  uint32_t buf = 0;                    /* buffer the next window lands in */
 
   /* ---- wave-uniform request pool ----
    * Requests are handed out in chunks of kPoolChunk.  Wave g of the grid owns
@@ -177,7 +220,10 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
    * counter (only touched when the batch has more chunks than waves), so the
    * launch does not start with every wave contending for one address. */
   const uint32_t nwaves = gridDim.x * WAVES;
-  const uint32_t nchunks = (p.n + kPoolChunk - 1) / kPoolChunk;
+  const uint32_t nchunks = (p.n + p.chunk - 1) / p.chunk;
+  uint32_t *chunk_list = reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave) + (tid >> 6) * kChunkCap;
+  uint32_t nlist = 0;                  /* wave-uniform */
+  bool deferred = false;               /* this lane left requests for the replay */
   uint32_t pool_next = 0, pool_end = 0;
   uint32_t next_chunk = blockIdx.x * WAVES + (tid >> 6);   /* wave-uniform */
   bool pool_dry = false;
@@ -190,22 +236,24 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
       if (pool_next >= pool_end) {
         uint32_t c = next_chunk;
         if (c == 0xffffffffu) {
-          if (nchunks <= nwaves) { pool_dry = true; break; }
+          if (nchunks <= nwaves || nlist == kChunkCap) { pool_dry = true; break; }
           uint32_t k = 0;
           if (lane == 0) k = atomicAdd(&p.work[0], 1u);
           c = nwaves + __builtin_amdgcn_readfirstlane(k);
         }
         next_chunk = 0xffffffffu;
-        if (c >= nchunks) { pool_dry = true; break; }
-        pool_next = c * kPoolChunk;
-        pool_end = min(pool_next + (uint32_t) kPoolChunk, p.n);
+        if (c >= nchunks || nlist == kChunkCap) { pool_dry = true; break; }
+        if (lane == 0) chunk_list[nlist] = c;
+        nlist++;
+        pool_next = c * p.chunk;
+        pool_end = min(pool_next + p.chunk, p.n);
       }
       uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
       uint32_t avail = pool_end - pool_next;
       if (!pend_ok && rank < avail) {
         pend = pool_next + rank;
-        pend_o0 = p.offsets[pend];
-        pend_o1 = p.offsets[pend + 1];
+        pend_o0 = GLOBAL(const uint64_t, p.offsets)[pend];
+        pend_o1 = GLOBAL(const uint64_t, p.offsets)[pend + 1];
         pend_ok = true;
       }
       pool_next += min((uint32_t) __popcll(want), avail);
@@ -220,30 +268,74 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
    *   bad   ERR at term < len, or max_headers overflow at a line start < len
    *   exact SLOW, a terminal at/after len, or no terminal by the end of the buffer
    */
+  /* one non-terminal event at request position ep: rhp_dfa.h dec_event, as
+   * straight-line selects (no divergent branches), plus the record store */
+  auto event = [&](uint32_t ep, rhp_hdr_t *hout) {
+    const uint32_t h23n = (d.h23 << 16) | (d.h01 >> 16);
+    const uint32_t h01n = (d.h01 << 16) | ep;
+    const uint32_t k = d.k;
+    const bool is_rl = k == 3, is_co = k == 4, is_eol = k == 6;
+    /* RL: history = RL, PE, PS, ME */
+    const uint32_t pe = h01n >> 16, ps = h23n & 0xffffu, me = h23n >> 16;
+    d.rl01 = is_rl ? (me | (ps << 16)) : d.rl01;
+    d.rl23 = is_rl ? ((pe - ps) | ((ep - pe - 9u) << 16)) : d.rl23;
+    d.h01 = is_rl ? ((h01n & 0xffff0000u) | (pe + 10u)) : h01n;
+    d.h23 = h23n;
+    /* CO: history = CO, prevLF; the max_headers check of the line start */
+    d.ovf = (is_co && d.nh == maxh && d.ovf == 0) ? (h01n >> 16) + 2u : d.ovf;
+    /* EOL: history = LF, VS, CO, prevLF */
+    const uint32_t vs = h01n >> 16, co = h23n & 0xffffu, prev = h23n >> 16;
+    const uint32_t lo = (prev + 1u) | ((co - prev - 1u) << 16);
+    const uint32_t hi = vs | ((ep - 1u - vs) << 16);
+    const uint32_t nh = d.nh + (is_eol ? 1u : 0u);
+    d.k = is_eol ? 4u : k + 1u;
+    d.nh = nh;
+    if (is_eol && nh <= maxh) {
+      if (nh & 1u) { rec_lo = lo; rec_hi = hi; }
+      else if (!(p.pad & 2)) store_pair(hout + nh - 2u, u32x4{rec_lo, rec_hi, lo, hi});
+    }
+  };
+
+  /*
+   * Decode the block's events and finalize cur when its outcome is known
+   * (decisions mirrored by rhp_emu.cpp):
+   *   ok    DONE at term < len
+   *   bad   ERR at term < len, or max_headers overflow at a line start < len
+   *   exact SLOW, a terminal at/after len, or no terminal by the end of the buffer
+   */
   auto decode = [&]() {
     if (!has) return;
     const uint32_t row = st;
     const bool slow = row == row_of(S_SLOW);
-    const bool term_ev = is_done_row(row) || is_err_row(row);   /* its last event is the terminal */
+    const bool term_ev = is_done_row(row) || is_err_row(row);
     uint32_t mlo = slow ? 0u : ev_lo, mhi = slow ? 0u : ev_hi;
     uint32_t term_pos = 0xffffffffu;
+    if (term_ev) {   /* the terminal is the block's last event: take it off the mask */
+      if (mhi) {
+        const uint32_t bt = 31u - __builtin_clz(mhi);
+        term_pos = (uint32_t) block_pos + 32u + bt;
+        mhi &= ~(1u << bt);
+      } else if (mlo) {
+        const uint32_t bt = 31u - __builtin_clz(mlo);
+        term_pos = (uint32_t) block_pos + bt;
+        mlo &= ~(1u << bt);
+      }
+    }
     rhp_hdr_t *hout = p.hdrs + (uint64_t) cur * maxh;
-    while (__ballot((mlo | mhi) != 0)) {
-      if ((mlo | mhi) != 0) {
-        uint32_t b;
-        if (mlo) { b = __builtin_ctz(mlo); mlo &= mlo - 1u; }
-        else { b = 32u + __builtin_ctz(mhi); mhi &= mhi - 1u; }
-        const uint32_t ep = (uint32_t) (block_pos + (int32_t) b);
-        if (term_ev && (mlo | mhi) == 0) {
-          term_pos = ep;
-        } else {
-          uint32_t lo, hi;
-          if (dec_event(d, ep, maxh, lo, hi)) {
-            if (d.nh & 1u) { rec_lo = lo; rec_hi = hi; }
-            else if (!(p.pad & 2)) store_pair(hout + d.nh - 2u, u32x4{rec_lo, rec_hi, lo, hi});
-          }
-          if (d.ovf) { mlo = mhi = 0; }
-        }
+    while (__ballot(mlo != 0)) {
+      if (mlo) {
+        const uint32_t bt = __builtin_ctz(mlo);
+        mlo &= mlo - 1u;
+        event((uint32_t) block_pos + bt, hout);
+        if (d.ovf) mlo = mhi = 0;
+      }
+    }
+    while (__ballot(mhi != 0)) {
+      if (mhi) {
+        const uint32_t bt = __builtin_ctz(mhi);
+        mhi &= mhi - 1u;
+        event((uint32_t) block_pos + 32u + bt, hout);
+        if (d.ovf) mhi = 0;
       }
     }
     const bool ovf = d.ovf != 0;
@@ -251,32 +343,26 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
     if (!fin) return;
     const bool ok = !ovf && is_done_row(row) && term_pos < cur_len;
     const bool bad = ovf ? d.ovf - 1u < cur_len : (is_err_row(row) && term_pos < cur_len);
+    rhp_req_t r = {};
+    r.minor_version = -1;
     if (ok) {
       if ((d.nh & 1u) && !(p.pad & 2)) store_one(hout + d.nh - 1u, u32x2{rec_lo, rec_hi});
-      rhp_req_t r;
       r.ret = (int32_t) term_pos + 1;
       r.method_len = (uint16_t) d.rl01;
       r.path_off = (uint16_t) (d.rl01 >> 16);
       r.path_len = (uint16_t) d.rl23;
-      r.method_off = 0;
       r.minor_version = (int8_t) (d.rl23 >> 16);
       r.num_headers = (uint16_t) d.nh;
-      r.flags = 0;
-      if (!(p.pad & 2)) p.reqs[cur] = r;
-      if (p.mode == RHP_MODE_HTTP) finish_http(p, cur, cur_off, cur_len, r);
+      r.flags = p.mode == RHP_MODE_HTTP ? (uint16_t) kDeferFrame : (uint16_t) 0;   /* framing: replay */
+      deferred |= p.mode == RHP_MODE_HTTP;
     } else if (bad) {
-      rhp_req_t r;
       r.ret = -1;
-      r.method_len = r.path_off = r.path_len = 0;
-      r.method_off = 0; r.minor_version = -1; r.num_headers = 0; r.flags = 0;
-      p.reqs[cur] = r;
-      if (p.mode == RHP_MODE_HTTP) {
-        rhp_http_t x = {-1, 0, 0, 0};
-        p.http[cur] = x;
-      }
+      if (p.mode == RHP_MODE_HTTP) store_http_bad(p.http + cur);
     } else {
-      finish_exact(p, cur, cur_off, cur_len);
+      r.flags = (uint16_t) kDeferExact;   /* exact path: replay */
+      deferred = true;
     }
+    if (!(p.pad & 2)) store_req(p.reqs + cur, r);
     has = false;
     st = park;
   };
@@ -288,6 +374,9 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
       const uint32_t c = (chunk[k >> 2] >> ((k & 3) * 8)) & 0xffu;
       st = *reinterpret_cast<const uint16_t *>(lds + st + c * 2u);
       ev |= (st >> kEventBit) << (base + k);
+      /* keep the scheduler from hoisting the byte extraction of all 64 steps
+       * (it would hold 64 VGPRs of precomputed offsets) */
+      if ((k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -309,8 +398,14 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
     RHP_STAMP(t0);
     /* [A] */
     const uint64_t p_o0 = pend_o0, p_o1 = pend_o1;
+    const uint32_t nw_kind_prev = nw_kind;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the window's LDS-DMA has landed */
+    {
+      const uint8_t *sb = lds + stage + (buf ^ kStageBuf);
 #pragma unroll
-    for (int q = 0; q < 4; q++) W[q] = NW[q];
+      for (int q = 0; q < 4; q++)
+        W[q] = nw_kind_prev ? *reinterpret_cast<const u32x4 *>(sb + stage_off(lane, q)) : u32x4{0, 0, 0, 0};
+    }
 #ifdef RHP_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     RHP_STAMP(t1); acc[0] += t1 - t0; t0 = t1;
@@ -349,11 +444,21 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
       nw_kind = 2;
     }
     {
-      /* p.pad bit 0 (experiment): read every window from the first 256 B of the
-       * batch (cache-resident) instead of the lane's own request */
-      const uint64_t src = (p.pad & 1) ? (nw_ptr & 192) : nw_ptr;
+      /* the wave fetches all 64 windows with 4 LDS-DMA loads, 16 windows of 64 B each */
+      const uint64_t src = nw_kind ? nw_ptr : ~(uint64_t) 0;
+      const uint32_t slo = (uint32_t) src, shi = (uint32_t) (src >> 32);
+      const uint32_t part = ((lane & 3u) - (lane >> 4)) & 3u;
 #pragma unroll
-      for (int q = 0; q < 4; q++) NW[q] = nw_kind ? load_chunk(p.bytes + src + 16 * q) : u32x4{0, 0, 0, 0};
+      for (int i = 0; i < 4; i++) {
+        const uint32_t w = 16u * i + (lane >> 2);
+        const uint32_t lo = __shfl(slo, (int) w), hi = __shfl(shi, (int) w);
+        const uint64_t a = ((uint64_t) hi << 32) | lo;
+        if (a != ~(uint64_t) 0)
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(p.bytes + a + 16u * part),
+                                           (__attribute__((address_space(3))) void *) (lds + stage + buf + 1024u * i),
+                                           16, 0, 0);
+      }
+      buf ^= kStageBuf;
     }
     if (!__ballot(has || nw_kind || pend_ok)) break;
 #ifdef RHP_STAMPS
@@ -383,6 +488,30 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
     g_stamps[w * 8 + 7] = t_exit - t_entry;
   }
 #endif
+
+  /* Replay: the rare paths run here, after the DFA loop, so none of their
+   * registers are live in it.  The wave walks the chunks it took, one request
+   * per lane, and finishes what finalize deferred: the exact scalar path, and
+   * http_read_request framing of DFA-parsed requests in http mode. */
+  if (__ballot(deferred)) {
+    for (uint32_t k = 0; k < nlist; k++) {
+      const uint32_t c = chunk_list[k];
+      const uint32_t lo = c * p.chunk, hi = min(lo + p.chunk, p.n);
+      for (uint32_t i = lo + lane; i < hi; i += 64) {
+        const uint32_t f = p.reqs[i].flags;
+        if (!(f & (kDeferExact | kDeferFrame))) continue;
+        const uint64_t off = p.offsets[i], len = p.offsets[i + 1] - off;
+        if (f & kDeferExact) {
+          finish_exact(p, i, off, len);
+        } else {
+          rhp_req_t r = p.reqs[i];
+          r.flags = 0;
+          finish_http(p, i, off, len, r);
+          p.reqs[i].flags = 0;
+        }
+      }
+    }
+  }
 
   /* the last workgroup out re-arms the work counters for the next launch, so a
    * step is exactly one kernel launch (no memset) */
@@ -415,7 +544,7 @@ int g_cus = 0;
 template <int WAVES>
 int launch_dfa(const Params &prm, hipStream_t s)
 {
-  const size_t lds_bytes = kLdsTable;
+  const size_t lds_bytes = kLdsTable + (size_t) WAVES * (kStageWave + 4 * kChunkCap);
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES>),
@@ -430,7 +559,16 @@ int launch_dfa(const Params &prm, hipStream_t s)
   uint32_t grid = (uint32_t) (g_cus * per_cu);
   uint32_t need = (prm.n + 64 * WAVES - 1) / (64 * WAVES);
   if (grid > need) grid = need > 0 ? need : 1;
-  hipLaunchKernelGGL(rhp_dfa_kernel<WAVES>, dim3(grid), dim3(WAVES * 64), lds_bytes, s, prm);
+  /* chunk size: >= 256 requests, and large enough that the pool runs dry before
+   * any wave has used its kChunkCap list entries twice over */
+  Params q = prm;
+  const uint64_t waves = (uint64_t) grid * WAVES;
+  uint64_t chunk = (2ull * prm.n + waves * kChunkCap - 1) / (waves * kChunkCap);
+  chunk = (chunk + 63) & ~63ull;
+  uint64_t floor_chunk = kPoolChunk;
+  if (const char *e = getenv("RHP_CHUNK")) floor_chunk = (uint64_t) atoi(e);   /* experiments */
+  q.chunk = (uint32_t) (chunk < floor_chunk ? floor_chunk : chunk);
+  hipLaunchKernelGGL(rhp_dfa_kernel<WAVES>, dim3(grid), dim3(WAVES * 64), lds_bytes, s, q);
   return (int) hipGetLastError();
 }
 
@@ -495,6 +633,7 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.n = b->n;
   prm.max_headers = b->max_headers;
   prm.mode = b->mode;
+  prm.chunk = kPoolChunk;
   {
     const char *e = getenv("RHP_EXPERIMENT");   /* timing experiments only: breaks results */
     prm.pad = e ? (uint32_t) atoi(e) : 0u;

@@ -23,6 +23,7 @@ bounded sample of the same workload.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -63,30 +64,46 @@ def traffic_from_profile(config_key: str):
 
 
 def cpu_baseline(cfg, seconds: float = 12.0):
-    """Oracle restatement ("port") on the host cores, bounded sample of the workload."""
+    """The reference CPU parser on the host cores, on a bounded sample of the workload.
+
+    Prefers the real reference (phr_parse_request compiled from the reference's
+    sources with its own -O3 flags into oracle/_ref/libref.so by oracle/Makefile,
+    kind "reference"); falls back to the from-scratch restatement (kind "port")
+    when that library is absent (it is built only where /root/reference exists)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from oracle_util import ORC_HDR, ORC_REQ, oracle
-    o = oracle()
+    from oracle_util import LIBREF, ORC_HDR, ORC_REQ, oracle
     n = 1 << 18
     buf, off = rhp.generate(cfg["gen"], n, cfg["seed"])
     hb = rhp.header_bytes(cfg["gen"], n, cfg["seed"])
-    reqs = np.zeros(n, dtype=ORC_REQ)
-    hdrs = np.zeros((n, cfg["maxh"]), dtype=ORC_HDR)
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    if os.path.exists(LIBREF):
+        ref = ctypes.CDLL(LIBREF)
+        ref.ref_phr_batch_mt.restype = ctypes.c_uint64
+        ref.ref_phr_batch_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        chk = ctypes.c_long(0)
+        run = lambda t, reps: ref.ref_phr_batch_mt(buf.ctypes.data, off.ctypes.data, n, cfg["maxh"], t, reps,
+                                                   ctypes.byref(chk))
+        kind, what = "reference", ("phr_parse_request of the reference (src/picohttpparser/picohttpparser.c, "
+                                   "gcc -O3 -march=x86-64-v3 as its Makefile.am:61 builds it, SSE4.2 path)")
+    else:
+        o = oracle()
+        reqs = np.zeros(n, dtype=ORC_REQ)
+        hdrs = np.zeros((n, cfg["maxh"]), dtype=ORC_HDR)
+        run = lambda t, reps: o.orc_phr_batch_mt(buf.ctypes.data, off.ctypes.data, n, cfg["maxh"],
+                                                 reqs.ctypes.data, hdrs.ctypes.data, t, reps)
+        kind, what = "port", "oracle/rhp_oracle.c phr_parse_request restatement (gcc -O3 -march=x86-64-v3)"
     out = {}
     for t in sorted({1, threads}):
-        o.orc_phr_batch_mt(buf.ctypes.data, off.ctypes.data, n, cfg["maxh"], reqs.ctypes.data, hdrs.ctypes.data, t, 1)
-        one = o.orc_phr_batch_mt(buf.ctypes.data, off.ctypes.data, n, cfg["maxh"], reqs.ctypes.data,
-                                 hdrs.ctypes.data, t, 1) / 1e9
+        run(t, 1)
+        one = run(t, 1) / 1e9
         reps = max(1, int(seconds / 2 / max(one, 1e-6)))
-        ns = o.orc_phr_batch_mt(buf.ctypes.data, off.ctypes.data, n, cfg["maxh"], reqs.ctypes.data,
-                                hdrs.ctypes.data, t, reps)
+        ns = run(t, reps)
         out[t] = (hb * reps / (ns / 1e9) / 2 ** 30, reps)
     v, reps = out[threads]
-    return {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+    return {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
             "value_1_thread": round(out[1][0], 3),
-            "sample": f"oracle/rhp_oracle.c phr_parse_request restatement, {n} requests of the same "
-                      f"workload x {reps} passes, {threads} pthreads (gcc -O3 -march=x86-64-v3)"}
+            "sample": f"{what}; {n} requests of the same workload x {reps} passes, {threads} pthreads"}
 
 
 def main():

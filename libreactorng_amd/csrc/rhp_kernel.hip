@@ -261,26 +261,18 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
     }
   };
 
-  /*
-   * Decode the block's events and finalize cur when its outcome is known
-   * (decisions mirrored by rhp_emu.cpp):
-   *   ok    DONE at term < len
-   *   bad   ERR at term < len, or max_headers overflow at a line start < len
-   *   exact SLOW, a terminal at/after len, or no terminal by the end of the buffer
-   */
-  /* one non-terminal event at request position ep: rhp_dfa.h dec_event, as
-   * straight-line selects (no divergent branches), plus the record store */
-  auto event = [&](uint32_t ep, rhp_hdr_t *hout) {
+  /* one non-terminal event at request position ep, for the lanes with `valid`:
+   * rhp_dfa.h dec_event as straight-line selects, so the event loop runs with a
+   * uniform exec mask (no per-lane branches, no PHI copies) except for the store */
+  auto event = [&](bool valid, uint32_t ep, rhp_hdr_t *hout) {
     const uint32_t h23n = (d.h23 << 16) | (d.h01 >> 16);
     const uint32_t h01n = (d.h01 << 16) | ep;
     const uint32_t k = d.k;
-    const bool is_rl = k == 3, is_co = k == 4, is_eol = k == 6;
+    const bool is_rl = valid && k == 3, is_co = valid && k == 4, is_eol = valid && k == 6;
     /* RL: history = RL, PE, PS, ME */
     const uint32_t pe = h01n >> 16, ps = h23n & 0xffffu, me = h23n >> 16;
     d.rl01 = is_rl ? (me | (ps << 16)) : d.rl01;
     d.rl23 = is_rl ? ((pe - ps) | ((ep - pe - 9u) << 16)) : d.rl23;
-    d.h01 = is_rl ? ((h01n & 0xffff0000u) | (pe + 10u)) : h01n;
-    d.h23 = h23n;
     /* CO: history = CO, prevLF; the max_headers check of the line start */
     d.ovf = (is_co && d.nh == maxh && d.ovf == 0) ? (h01n >> 16) + 2u : d.ovf;
     /* EOL: history = LF, VS, CO, prevLF */
@@ -288,12 +280,16 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
     const uint32_t lo = (prev + 1u) | ((co - prev - 1u) << 16);
     const uint32_t hi = vs | ((ep - 1u - vs) << 16);
     const uint32_t nh = d.nh + (is_eol ? 1u : 0u);
-    d.k = is_eol ? 4u : k + 1u;
+    d.h01 = !valid ? d.h01 : is_rl ? ((h01n & 0xffff0000u) | (pe + 10u)) : h01n;
+    d.h23 = valid ? h23n : d.h23;
+    d.k = !valid ? k : is_eol ? 4u : k + 1u;
     d.nh = nh;
-    if (is_eol && nh <= maxh) {
-      if (nh & 1u) { rec_lo = lo; rec_hi = hi; }
-      else if (!(p.pad & 2)) store_pair(hout + nh - 2u, u32x4{rec_lo, rec_hi, lo, hi});
-    }
+    const bool keep = is_eol && nh <= maxh;
+    const bool odd = (nh & 1u) != 0;
+    const uint32_t plo = rec_lo, phi = rec_hi;
+    rec_lo = keep && odd ? lo : rec_lo;
+    rec_hi = keep && odd ? hi : rec_hi;
+    if (keep && !odd && !(p.pad & 2)) store_pair(hout + nh - 2u, u32x4{plo, phi, lo, hi});
   };
 
   /*
@@ -323,20 +319,19 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
     }
     rhp_hdr_t *hout = p.hdrs + (uint64_t) cur * maxh;
     while (__ballot(mlo != 0)) {
-      if (mlo) {
-        const uint32_t bt = __builtin_ctz(mlo);
-        mlo &= mlo - 1u;
-        event((uint32_t) block_pos + bt, hout);
-        if (d.ovf) mlo = mhi = 0;
-      }
+      const bool valid = mlo != 0;
+      const uint32_t bt = __builtin_ctz(mlo | 0x80000000u);
+      mlo &= mlo - 1u;
+      event(valid, (uint32_t) block_pos + bt, hout);
+      mlo = d.ovf ? 0u : mlo;
     }
+    mhi = d.ovf ? 0u : mhi;
     while (__ballot(mhi != 0)) {
-      if (mhi) {
-        const uint32_t bt = __builtin_ctz(mhi);
-        mhi &= mhi - 1u;
-        event((uint32_t) block_pos + 32u + bt, hout);
-        if (d.ovf) mhi = 0;
-      }
+      const bool valid = mhi != 0;
+      const uint32_t bt = __builtin_ctz(mhi | 0x80000000u);
+      mhi &= mhi - 1u;
+      event(valid, (uint32_t) block_pos + 32u + bt, hout);
+      mhi = d.ovf ? 0u : mhi;
     }
     const bool ovf = d.ovf != 0;
     const bool fin = ovf || slow || term_ev || pos >= (int32_t) cur_len;

@@ -127,3 +127,60 @@ void ref_http_batch(uint8_t *bytes, const uint64_t *offsets, uint32_t n,
     }
   }
 }
+
+/* ---- CPU baseline: the reference parser itself, timed on the host cores ----
+ * Each thread runs phr_parse_request (the reference's own -O3 build flags, see
+ * oracle/Makefile) over its contiguous share of the batch, reps times, exactly
+ * as libreactor's http_read_request calls it; returns elapsed ns. */
+#include <pthread.h>
+#include <time.h>
+
+struct ref_mt_arg {
+  const uint8_t *bytes;
+  const uint64_t *offsets;
+  uint32_t lo, hi, max_headers;
+  int reps;
+  long sum;
+};
+
+static void *ref_mt_worker(void *p)
+{
+  struct ref_mt_arg *a = p;
+  struct phr_header tmp[256];
+  long sum = 0;
+  for (int rep = 0; rep < a->reps; rep++)
+    for (uint32_t i = a->lo; i < a->hi; i++) {
+      const char *method, *path;
+      size_t method_len, path_len, num = a->max_headers;
+      int minor;
+      sum += phr_parse_request((const char *) a->bytes + a->offsets[i], a->offsets[i + 1] - a->offsets[i],
+                               &method, &method_len, &path, &path_len, &minor, tmp, &num, 0);
+    }
+  a->sum = sum;
+  return NULL;
+}
+
+uint64_t ref_phr_batch_mt(const uint8_t *bytes, const uint64_t *offsets, uint32_t n, uint32_t max_headers,
+                          int threads, int reps, long *checksum)
+{
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  if (max_headers > 256) max_headers = 256;
+  pthread_t tid[256];
+  struct ref_mt_arg args[256];
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int t = 0; t < threads; t++) {
+    args[t] = (struct ref_mt_arg) {bytes, offsets, (uint32_t) ((uint64_t) n * t / threads),
+                                   (uint32_t) ((uint64_t) n * (t + 1) / threads), max_headers, reps, 0};
+    pthread_create(&tid[t], NULL, ref_mt_worker, &args[t]);
+  }
+  long sum = 0;
+  for (int t = 0; t < threads; t++) {
+    pthread_join(tid[t], NULL);
+    sum += args[t].sum;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  if (checksum) *checksum = sum;
+  return (uint64_t) (t1.tv_sec - t0.tv_sec) * 1000000000ull + (uint64_t) (t1.tv_nsec - t0.tv_nsec);
+}

@@ -8,29 +8,32 @@
  *
  * Events.  Rows live in two LDS ranges: plain rows below kEventRow and event
  * rows at/above it, so bit 14 of an entry says "this transition is an event".
- * The kernel ORs that bit into a 64-bit per-block mask (two VALU ops per step,
- * no LDS write) and decodes the mask once per 64-byte block.  For a request the
- * fast path accepts, the event sequence is fixed by the grammar:
+ * The kernel ORs that bit into a per-block mask (two VALU ops per step, no LDS
+ * write) and decodes the mask once per block.  For a request the fast path
+ * accepts, the event sequence is fixed by the grammar:
  *
- *   ME  PS  PE  RL          request line: method end (1st SP), path start,
- *                           path end (2nd SP), RL = the CR of "HTTP/1.0\r\n"
- *                           or the LF of "HTTP/1.1\r\n" (so the position
- *                           encodes the minor version: RL - PE = 9 or 10)
- *   { CO  VS  EOL }*        per header line: colon, value start (first
- *                           non-OWS byte after the colon, the CR for an empty
- *                           value), the LF that ends the line
+ *   ME  PE  RL              request line: method end (the SP; the path starts
+ *                           right after it), path end (the next SP), RL = the
+ *                           CR of "HTTP/1.0\r\n" or the LF of "HTTP/1.1\r\n" (so
+ *                           the position encodes the minor version: RL - PE =
+ *                           9 or 10)
+ *   { CO  EOL }*            per header line: the colon (the value starts two
+ *                           bytes later, after its one SP) and the LF that ends
+ *                           the line
  *   T                       terminal: the final LF (DONE) or the byte at which
  *                           the reference returns -1 (ERR)
  *
  * Each event shifts its position into a 4-deep u16 history, which then holds
- * everything a record needs (method start is 0: a leading empty line goes to
- * the exact path).  The DFA only decides what it can decide without knowing
- * where the buffer ends: a terminal is the reference's answer iff its byte
- * lies before `len`; constructs that are rare or end-dependent go to the SLOW
- * terminal and are re-parsed by the exact scalar path (rhp_scalar.h): leading
- * CRLF, empty method, extra SP before the version, version other than
- * HTTP/1.0 / HTTP/1.1, bare LF line ends, OWS before a CR (value trimming),
- * obs-fold continuation lines, requests longer than kFastMaxLen.
+ * everything a record needs.  The DFA only decides what it can decide without
+ * knowing where the buffer ends: a terminal is the reference's answer iff its
+ * byte lies before `len`; constructs that are rare in real traffic or whose
+ * answer depends on where the buffer ends go to the SLOW terminal and are
+ * re-parsed by the exact scalar path (rhp_scalar.h): a leading empty line, an
+ * empty method, more than one SP between request-line fields, versions other
+ * than HTTP/1.0 and HTTP/1.1, bare-LF line ends, anything but exactly one SP
+ * after a header colon (":v", ":\tv", ":  v", ":\r\n"), OWS before a CR
+ * (value trimming), obs-fold continuation lines, requests longer than
+ * kFastMaxLen.
  */
 #ifndef RHP_DFA_H
 #define RHP_DFA_H
@@ -49,20 +52,17 @@ enum State : uint32_t {
   /* plain rows (no event on entry) */
   S_DONE = 0, S_ERR, S_SLOW,                   /* terminals */
   S_SKIP3, S_SKIP2, S_SKIP1,                   /* leading bytes of an unaligned window */
-  S_METHOD0, S_METHOD, S_SP1, S_PATH,
+  S_METHOD0, S_METHOD, S_PATH0, S_PATH,
   S_V1, S_V2, S_V3, S_V4, S_V5, S_V6, S_V7, S_V8_0, S_V8_1, S_CRLF_RL,
-  S_LINE0, S_NAME, S_COLON, S_VALUE, S_VWS, S_VCR, S_END_CR,
+  S_LINE0, S_NAME, S_VAL0, S_VALUE, S_VWS, S_VCR, S_END_CR,
   S_NUM_PLAIN,
   /* event rows (an event fires on the transition that enters them) */
   S_DONE_E = S_NUM_PLAIN, S_ERR_E,             /* terminal events */
   S_SP1_E,       /* ME */
-  S_PATH_E,      /* PS */
   S_SP2_E,       /* PE */
   S_CRLF_RL_E,   /* RL at the CR (HTTP/1.0) */
   S_LINE0_E,     /* RL at the LF (HTTP/1.1) */
   S_COLON_E,     /* CO */
-  S_VALUE_E,     /* VS */
-  S_VCR_E,       /* VS at the CR of an empty value */
   S_LINE_E,      /* EOL */
   S_COUNT
 };
@@ -114,10 +114,10 @@ constexpr uint32_t step(uint32_t s, uint32_t c)
   case S_METHOD:
     if (c == ' ') return S_SP1_E;
     return c_ctl(c) ? S_ERR_E : S_METHOD;
-  case S_SP1: case S_SP1_E:   /* do ++buf while SP (:356-358), then the path token (:359) */
-    if (c == ' ') return S_SP1;
-    return c_ctl(c) ? S_ERR_E : S_PATH_E;
-  case S_PATH: case S_PATH_E:
+  case S_SP1_E:     /* SP skip (:356-358): a second SP -> exact path; then the path token (:359) */
+    if (c == ' ') return S_SLOW;
+    return c_ctl(c) ? S_ERR_E : S_PATH;
+  case S_PATH:
     if (c == ' ') return S_SP2_E;
     return c_ctl(c) ? S_ERR_E : S_PATH;
   case S_SP2_E:     /* "HTTP/1." + digit (:245-261) right after one SP */
@@ -148,12 +148,14 @@ constexpr uint32_t step(uint32_t s, uint32_t c)
   case S_NAME:      /* name bytes must be tchar up to ':' (:297-310) */
     if (c == ':') return S_COLON_E;
     return c_tchar(c) ? S_NAME : S_ERR_E;
-  case S_COLON: case S_COLON_E:   /* OWS after ':' (:312-317), then get_token_to_eol (:134-195) */
-    if (c_ows(c)) return S_COLON;
-    if (c == '\r') return S_VCR_E;
-    if (c == '\n') return S_SLOW;
-    return c_ctl(c) ? S_ERR_E : S_VALUE_E;
-  case S_VALUE: case S_VALUE_E:
+  case S_COLON_E:   /* OWS after ':' (:312-317): exactly one SP on the fast path */
+    if (c == ' ') return S_VAL0;
+    return c_ctl(c) && c != '\t' && c != '\r' && c != '\n' ? S_ERR_E : S_SLOW;
+  case S_VAL0:      /* first value byte, get_token_to_eol (:134-195) */
+    if (c_ows(c) || c == '\n') return S_SLOW;
+    if (c == '\r') return S_VCR;
+    return c_ctl(c) ? S_ERR_E : S_VALUE;
+  case S_VALUE:
     if (c_ows(c)) return S_VWS;
     if (c == '\r') return S_VCR;
     if (c == '\n') return S_SLOW;
@@ -162,7 +164,7 @@ constexpr uint32_t step(uint32_t s, uint32_t c)
     if (c_ows(c)) return S_VWS;
     if (c == '\r' || c == '\n') return S_SLOW;
     return c_ctl(c) ? S_ERR_E : S_VALUE;
-  case S_VCR: case S_VCR_E: return c == '\n' ? S_LINE_E : S_ERR_E;
+  case S_VCR: return c == '\n' ? S_LINE_E : S_ERR_E;
   case S_END_CR:    /* empty line ends the headers (:268-275) */
     return c == '\n' ? S_DONE_E : S_ERR_E;
   default: return S_SLOW;
@@ -188,7 +190,7 @@ constexpr Table make_table()
  */
 struct Dec {
   uint32_t h01, h23;
-  uint32_t k;       /* events consumed: 0..3 request line, then 4,5,6 = CO, VS, EOL */
+  uint32_t k;       /* events consumed: 0..2 request line, then 3,4 = CO, EOL */
   uint32_t nh;      /* header lines completed */
   uint32_t rl01;    /* method_len | path_off << 16 */
   uint32_t rl23;    /* path_len | minor << 16 */
@@ -215,33 +217,29 @@ RHP_DHD inline bool dec_event(Dec &d, uint32_t p, uint32_t maxh, uint32_t &lo, u
 {
   d.h23 = (d.h23 << 16) | (d.h01 >> 16);
   d.h01 = (d.h01 << 16) | p;
-  if (d.k < 3) {
+  if (d.k < 2) {
     d.k++;
     return false;
   }
-  if (d.k == 3) {   /* RL: history = RL, PE, PS, ME */
-    const uint32_t pe = d.h01 >> 16, ps = d.h23 & 0xffffu, me = d.h23 >> 16;
+  if (d.k == 2) {   /* RL: history = RL, PE, ME */
+    const uint32_t pe = d.h01 >> 16, me = d.h23 & 0xffffu;
     const uint32_t minor = p - pe - 9u;   /* 0 (event at the CR) or 1 (at the LF) */
-    d.rl01 = me | (ps << 16);
-    d.rl23 = (pe - ps) | (minor << 16);
+    d.rl01 = me | ((me + 1u) << 16);
+    d.rl23 = (pe - me - 1u) | (minor << 16);
     d.h01 = (d.h01 & 0xffff0000u) | (pe + 10u);   /* e0 := the LF that ends the request line */
+    d.k = 3;
+    return false;
+  }
+  if (d.k == 3) {   /* CO: history = CO, prevLF, ... */
+    if (d.nh == maxh && d.ovf == 0) d.ovf = 1u + (d.h01 >> 16) + 1u;
     d.k = 4;
     return false;
   }
-  if (d.k == 4) {   /* CO: history = CO, prevLF, ... */
-    if (d.nh == maxh && d.ovf == 0) d.ovf = 1u + (d.h01 >> 16) + 1u;
-    d.k = 5;
-    return false;
-  }
-  if (d.k == 5) {   /* VS */
-    d.k = 6;
-    return false;
-  }
-  /* EOL: history = LF, VS, CO, prevLF */
-  const uint32_t lf = p, vs = d.h01 >> 16, co = d.h23 & 0xffffu, prev = d.h23 >> 16;
+  /* EOL: history = LF, CO, prevLF */
+  const uint32_t lf = p, co = d.h01 >> 16, prev = d.h23 & 0xffffu;
   lo = (prev + 1u) | ((co - prev - 1u) << 16);
-  hi = vs | ((lf - 1u - vs) << 16);
-  d.k = 4;
+  hi = (co + 2u) | ((lf - co - 3u) << 16);
+  d.k = 3;
   d.nh++;
   return d.nh <= maxh;
 }

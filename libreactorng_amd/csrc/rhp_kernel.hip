@@ -49,15 +49,28 @@ struct Params {
   uint32_t max_headers;
   uint32_t mode;
   uint32_t pad;
-  uint32_t chunk;   /* requests per pool chunk (host: >= 256, sized so no wave needs > kChunkCap) */
+  uint32_t chunk;   /* requests per sub-chunk a wave takes */
+  uint32_t span;    /* requests per workgroup */
 };
 
+#ifndef RHP_BLOCK
+#define RHP_BLOCK 64
+#endif
+#ifndef RHP_SINGLE_STAGE
+#define RHP_SINGLE_STAGE 0
+#endif
+#ifndef RHP_MIN_WAVES_PER_SIMD
+#define RHP_MIN_WAVES_PER_SIMD 1
+#endif
 enum : uint32_t {
   kPoolChunk = 256,
-  kBlock = 64,
+  kBlock = RHP_BLOCK,                            /* window bytes per lane per loop iteration */
+  kHalves = kBlock / 64,                         /* 64-byte halves per window */
+  kEvWords = kBlock / 32,
   kLdsTable = (kTableBytes + 1023u) & ~1023u,   /* staging starts 1 KiB aligned */
   kStageBuf = 64 * kBlock,                       /* one window per lane */
-  kStageWave = 2 * kStageBuf,                    /* double-buffered */
+  kDoubleStage = kHalves == 1 && !RHP_SINGLE_STAGE,
+  kStageWave = kDoubleStage ? 2 * kStageBuf : kStageBuf,   /* double-buffered, or refilled right after it is read */
   kChunkCap = 32,                                /* chunks one wave may take (its replay list) */
   kDeferExact = 0x8000u,                         /* reqs[i].flags while deferred (kernel-internal) */
   kDeferFrame = 0x4000u
@@ -70,8 +83,11 @@ enum : uint32_t {
  * makes each lane's four ds_read_b128 of its own window bank-conflict free. */
 __device__ __forceinline__ uint32_t stage_off(uint32_t w, uint32_t q)
 {
+#ifdef RHP_OWN_WINDOW
+  return q * 1024u + w * 16u;
+#endif
   const uint32_t u = w & 15u;
-  return (w >> 4) * 1024u + u * 64u + ((q + (u >> 2)) & 3u) * 16u;
+  return (q >> 2) * 4096u + (w >> 4) * 1024u + u * 64u + ((q + (u >> 2)) & 3u) * 16u;
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -95,9 +111,10 @@ __device__ __forceinline__ u32x4 load_chunk(const uint8_t *p)
   return *reinterpret_cast<const u32x4a4 *>(p);
 }
 
-/* Exact scalar path for one request (phr or http mode).  Not inlined: it is the
- * rare path, and keeping it out of the DFA loop keeps the loop's registers low. */
-__device__ __noinline__ void finish_exact(const Params &p, uint32_t i, uint64_t off, uint64_t len)
+/* Exact scalar path for one request (phr or http mode).  Only called from the
+ * post-loop replay, where inlining it lets it reuse the loop's dead registers
+ * (a call there costs ~14 VGPRs of calling-convention overhead). */
+__device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64_t off, uint64_t len)
 {
 #ifdef RHP_EXPERIMENT_NO_EXACT
   p.reqs[i].ret = -9;
@@ -128,7 +145,7 @@ __device__ __noinline__ void finish_exact(const Params &p, uint32_t i, uint64_t 
 }
 
 /* http_read_request framing of a request the DFA parsed (http mode only) */
-__device__ __noinline__ void finish_http(const Params &p, uint32_t i, uint64_t off, uint64_t len, rhp_req_t r)
+__device__ __forceinline__ void finish_http(const Params &p, uint32_t i, uint64_t off, uint64_t len, rhp_req_t r)
 {
   http_frame(p.bytes_rw + off, len, r, p.hdrs + (uint64_t) i * p.max_headers, &p.http[i]);
 }
@@ -137,6 +154,15 @@ __device__ __noinline__ void finish_http(const Params &p, uint32_t i, uint64_t o
  * the hot stores go through explicit global-address-space pointers so they are
  * global_store (VM counter only), not flat_store (VM + LGKM). */
 #define GLOBAL(T, x) ((__attribute__((address_space(1))) T *) (x))
+
+/* ev |= event bit of entry st at bit position `bit`.  Written as asm so the
+ * compiler cannot reassociate a block's ORs into one tree at its end, which
+ * would keep every step's entry alive in its own VGPR. */
+__device__ __forceinline__ void ev_or(uint32_t &ev, uint32_t st, uint32_t bit)
+{
+  uint32_t t;
+  asm("v_lshrrev_b32 %1, 14, %2\n\tv_lshl_or_b32 %0, %1, %3, %0" : "+v"(ev), "=&v"(t) : "v"(st), "s"(bit));
+}
 
 /* a 16-byte header-record pair, or a single record, at 4-byte alignment */
 __device__ __forceinline__ void store_pair(rhp_hdr_t *dst, u32x4 v)
@@ -172,7 +198,7 @@ __device__ __forceinline__ void store_http_bad(rhp_http_t *dst)
  * table.  Persistent: grid = workgroups resident on the device.
  */
 template <int WAVES>
-__global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
+__global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_kernel(Params p)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid = threadIdx.x;
@@ -187,6 +213,7 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
     const u32x4 *src = reinterpret_cast<const u32x4 *>(&g_table);
     u32x4 *dst = reinterpret_cast<u32x4 *>(lds);
     for (uint32_t k = tid; k < kTableBytes / 16; k += WAVES * 64) dst[k] = src[k];
+    if (tid == 0) *reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * (kStageWave + 4 * kChunkCap)) = 0;
   }
   __syncthreads();
 
@@ -196,7 +223,9 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
   /* ---- lane state ---- */
   uint32_t st = park;                  /* LDS offset of the current state's row (= the last entry) */
   int32_t pos = 0, block_pos = 0;      /* request-relative position of the next byte / of the block */
-  uint32_t ev_lo = 0, ev_hi = 0;       /* events of the block just stepped */
+  uint32_t ev[kEvWords];               /* events of the block just stepped */
+#pragma unroll
+  for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
   bool has = false;                    /* cur is being parsed */
   uint32_t cur = 0, cur_len = 0;
   uint64_t cur_off = 0, cur_ptr = 0;   /* cur_ptr: byte offset of the window in W */
@@ -214,18 +243,18 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
   const uint32_t stage = kLdsTable + (tid >> 6) * kStageWave;   /* this wave's two buffers */
   uint32_t buf = 0;                    /* buffer the next window lands in */
 
-  /* ---- wave-uniform request pool ----
-   * Requests are handed out in chunks of kPoolChunk.  Wave g of the grid owns
-   * chunk g outright; chunks past the grid's first round come from one atomic
-   * counter (only touched when the batch has more chunks than waves), so the
-   * launch does not start with every wave contending for one address. */
-  const uint32_t nwaves = gridDim.x * WAVES;
-  const uint32_t nchunks = (p.n + p.chunk - 1) / p.chunk;
+  /* ---- request pool ----
+   * Workgroup g owns requests [g*span, (g+1)*span) (host: span = n / grid); its
+   * waves pull sub-chunks of p.chunk requests from an LDS counter, so the waves
+   * of a CU balance among themselves and no global atomic is ever touched.
+   * Each wave records its sub-chunks (at most kChunkCap; the host sizes p.chunk
+   * so the workgroup's range fits 16x over) for the post-loop replay. */
+  const uint32_t wg_lo = min(blockIdx.x * p.span, p.n), wg_hi = min(wg_lo + p.span, p.n);
   uint32_t *chunk_list = reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave) + (tid >> 6) * kChunkCap;
+  uint32_t *wg_counter = reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * (kStageWave + 4 * kChunkCap));
   uint32_t nlist = 0;                  /* wave-uniform */
   bool deferred = false;               /* this lane left requests for the replay */
   uint32_t pool_next = 0, pool_end = 0;
-  uint32_t next_chunk = blockIdx.x * WAVES + (tid >> 6);   /* wave-uniform */
   bool pool_dry = false;
 
   /* give every lane without a pending request one from the pool; the offsets
@@ -234,26 +263,25 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
     uint64_t want = __ballot(!pend_ok);
     while (want && !pool_dry) {
       if (pool_next >= pool_end) {
-        uint32_t c = next_chunk;
-        if (c == 0xffffffffu) {
-          if (nchunks <= nwaves || nlist == kChunkCap) { pool_dry = true; break; }
-          uint32_t k = 0;
-          if (lane == 0) k = atomicAdd(&p.work[0], 1u);
-          c = nwaves + __builtin_amdgcn_readfirstlane(k);
-        }
-        next_chunk = 0xffffffffu;
-        if (c >= nchunks || nlist == kChunkCap) { pool_dry = true; break; }
-        if (lane == 0) chunk_list[nlist] = c;
+        if (nlist == kChunkCap) { pool_dry = true; break; }
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(wg_counter, 1u);
+        c = __builtin_amdgcn_readfirstlane(c);
+        const uint32_t lo = wg_lo + c * p.chunk;
+        if (c >= (wg_hi - wg_lo + p.chunk - 1) / p.chunk) { pool_dry = true; break; }
+        if (lane == 0) chunk_list[nlist] = lo;
         nlist++;
-        pool_next = c * p.chunk;
-        pool_end = min(pool_next + p.chunk, p.n);
+        pool_next = lo;
+        pool_end = min(lo + p.chunk, wg_hi);
       }
       uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
       uint32_t avail = pool_end - pool_next;
       if (!pend_ok && rank < avail) {
         pend = pool_next + rank;
-        pend_o0 = GLOBAL(const uint64_t, p.offsets)[pend];
-        pend_o1 = GLOBAL(const uint64_t, p.offsets)[pend + 1];
+        typedef uint64_t u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
+        const u64x2a8 o = *GLOBAL(const u64x2a8, p.offsets + pend);   /* offsets[pend], offsets[pend+1] */
+        pend_o0 = o[0];
+        pend_o1 = o[1];
         pend_ok = true;
       }
       pool_next += min((uint32_t) __popcll(want), avail);
@@ -261,35 +289,35 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
     }
   };
 
-  /* one non-terminal event at request position ep, for the lanes with `valid`:
-   * rhp_dfa.h dec_event as straight-line selects, so the event loop runs with a
-   * uniform exec mask (no per-lane branches, no PHI copies) except for the store */
+  /* one non-terminal event at request position ep, for the lanes with `valid`
+   * (rhp_dfa.h dec_event): the history shift and the event counter are
+   * straight-line; the request-line record (once per request) and the header
+   * record (every second event) are branches taken only by the lanes concerned */
   auto event = [&](bool valid, uint32_t ep, rhp_hdr_t *hout) {
-    const uint32_t h23n = (d.h23 << 16) | (d.h01 >> 16);
-    const uint32_t h01n = (d.h01 << 16) | ep;
     const uint32_t k = d.k;
-    const bool is_rl = valid && k == 3, is_co = valid && k == 4, is_eol = valid && k == 6;
-    /* RL: history = RL, PE, PS, ME */
-    const uint32_t pe = h01n >> 16, ps = h23n & 0xffffu, me = h23n >> 16;
-    d.rl01 = is_rl ? (me | (ps << 16)) : d.rl01;
-    d.rl23 = is_rl ? ((pe - ps) | ((ep - pe - 9u) << 16)) : d.rl23;
-    /* CO: history = CO, prevLF; the max_headers check of the line start */
-    d.ovf = (is_co && d.nh == maxh && d.ovf == 0) ? (h01n >> 16) + 2u : d.ovf;
-    /* EOL: history = LF, VS, CO, prevLF */
-    const uint32_t vs = h01n >> 16, co = h23n & 0xffffu, prev = h23n >> 16;
-    const uint32_t lo = (prev + 1u) | ((co - prev - 1u) << 16);
-    const uint32_t hi = vs | ((ep - 1u - vs) << 16);
-    const uint32_t nh = d.nh + (is_eol ? 1u : 0u);
-    d.h01 = !valid ? d.h01 : is_rl ? ((h01n & 0xffff0000u) | (pe + 10u)) : h01n;
-    d.h23 = valid ? h23n : d.h23;
-    d.k = !valid ? k : is_eol ? 4u : k + 1u;
-    d.nh = nh;
-    const bool keep = is_eol && nh <= maxh;
-    const bool odd = (nh & 1u) != 0;
-    const uint32_t plo = rec_lo, phi = rec_hi;
-    rec_lo = keep && odd ? lo : rec_lo;
-    rec_hi = keep && odd ? hi : rec_hi;
-    if (keep && !odd && !(p.pad & 2)) store_pair(hout + nh - 2u, u32x4{plo, phi, lo, hi});
+    if (valid) {
+      d.h23 = (d.h23 << 16) | (d.h01 >> 16);
+      d.h01 = (d.h01 << 16) | ep;
+      d.k = k == 4 ? 3u : k + 1u;
+      /* CO: history = CO, prevLF; the max_headers check of the line start */
+      if (k == 3 && d.nh == maxh && d.ovf == 0) d.ovf = (d.h01 >> 16) + 2u;
+    }
+    if (valid && k == 2) {   /* RL: history = RL, PE, ME */
+      const uint32_t pe = d.h01 >> 16, me = d.h23 & 0xffffu;
+      d.rl01 = me | ((me + 1u) << 16);
+      d.rl23 = (pe - me - 1u) | ((ep - pe - 9u) << 16);
+      d.h01 = (d.h01 & 0xffff0000u) | (pe + 10u);
+    }
+    if (valid && k == 4) {   /* EOL: history = LF, CO, prevLF */
+      const uint32_t co = d.h01 >> 16, prev = d.h23 & 0xffffu;
+      const uint32_t lo = (prev + 1u) | ((co - prev - 1u) << 16);
+      const uint32_t hi = (co + 2u) | ((ep - co - 3u) << 16);
+      const uint32_t nh = ++d.nh;
+      if (nh <= maxh) {
+        if (nh & 1u) { rec_lo = lo; rec_hi = hi; }
+        else if (!(p.pad & 2)) store_pair(hout + nh - 2u, u32x4{rec_lo, rec_hi, lo, hi});
+      }
+    }
   };
 
   /*
@@ -304,34 +332,33 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
     const uint32_t row = st;
     const bool slow = row == row_of(S_SLOW);
     const bool term_ev = is_done_row(row) || is_err_row(row);
-    uint32_t mlo = slow ? 0u : ev_lo, mhi = slow ? 0u : ev_hi;
+    uint32_t m[kEvWords];
+#pragma unroll
+    for (int w = 0; w < (int) kEvWords; w++) m[w] = slow ? 0u : ev[w];
     uint32_t term_pos = 0xffffffffu;
     if (term_ev) {   /* the terminal is the block's last event: take it off the mask */
-      if (mhi) {
-        const uint32_t bt = 31u - __builtin_clz(mhi);
-        term_pos = (uint32_t) block_pos + 32u + bt;
-        mhi &= ~(1u << bt);
-      } else if (mlo) {
-        const uint32_t bt = 31u - __builtin_clz(mlo);
-        term_pos = (uint32_t) block_pos + bt;
-        mlo &= ~(1u << bt);
+      bool found = false;
+#pragma unroll
+      for (int w = (int) kEvWords - 1; w >= 0; w--) {
+        if (!found && m[w]) {
+          const uint32_t bt = 31u - __builtin_clz(m[w]);
+          term_pos = (uint32_t) block_pos + 32u * w + bt;
+          m[w] &= ~(1u << bt);
+          found = true;
+        }
       }
     }
     rhp_hdr_t *hout = p.hdrs + (uint64_t) cur * maxh;
-    while (__ballot(mlo != 0)) {
-      const bool valid = mlo != 0;
-      const uint32_t bt = __builtin_ctz(mlo | 0x80000000u);
-      mlo &= mlo - 1u;
-      event(valid, (uint32_t) block_pos + bt, hout);
-      mlo = d.ovf ? 0u : mlo;
-    }
-    mhi = d.ovf ? 0u : mhi;
-    while (__ballot(mhi != 0)) {
-      const bool valid = mhi != 0;
-      const uint32_t bt = __builtin_ctz(mhi | 0x80000000u);
-      mhi &= mhi - 1u;
-      event(valid, (uint32_t) block_pos + 32u + bt, hout);
-      mhi = d.ovf ? 0u : mhi;
+#pragma unroll
+    for (int w = 0; w < (int) kEvWords; w++) {
+      uint32_t mw = d.ovf ? 0u : m[w];
+      while (__ballot(mw != 0)) {
+        const bool valid = mw != 0;
+        const uint32_t bt = __builtin_ctz(mw | 0x80000000u);
+        mw &= mw - 1u;
+        event(valid, (uint32_t) block_pos + 32u * w + bt, hout);
+        mw = d.ovf ? 0u : mw;
+      }
     }
     const bool ovf = d.ovf != 0;
     const bool fin = ovf || slow || term_ev || pos >= (int32_t) cur_len;
@@ -368,11 +395,47 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
     for (int k = 0; k < 16; k++) {
       const uint32_t c = (chunk[k >> 2] >> ((k & 3) * 8)) & 0xffu;
       st = *reinterpret_cast<const uint16_t *>(lds + st + c * 2u);
-      ev |= (st >> kEventBit) << (base + k);
+      ev_or(ev, st, base + k);
       /* keep the scheduler from hoisting the byte extraction of all 64 steps
        * (it would hold 64 VGPRs of precomputed offsets) */
       if ((k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
+  };
+
+  /* half h of the lane's window from the staging buffer (zeros for an idle lane) */
+  auto read_half = [&](uint32_t kind, int h) {
+    const uint8_t *sb = lds + stage + (kDoubleStage ? (buf ^ kStageBuf) : 0u);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      W[q] = kind ? *reinterpret_cast<const u32x4 *>(sb + stage_off(lane, 4 * h + q)) : u32x4{0, 0, 0, 0};
+  };
+
+  /* LDS-DMA of half h of every lane's next window (nw_ptr / nw_kind) */
+  auto issue_half = [&](int h) {
+    uint8_t *db = lds + stage + (kDoubleStage ? buf : 4096u * h);
+#ifdef RHP_OWN_WINDOW
+    /* experiment: every lane fetches its own window (lane-linear) */
+    if (nw_kind) {
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(p.bytes + nw_ptr + 64u * h + 16u * i),
+                                         (__attribute__((address_space(3))) void *) (db + 1024u * i), 16, 0, 0);
+    }
+#else
+    /* the wave fetches all 64 windows with 4 LDS-DMA loads, 16 windows of 64 B each */
+    const uint64_t src = nw_kind ? nw_ptr + 64u * h : ~(uint64_t) 0;
+    const uint32_t slo = (uint32_t) src, shi = (uint32_t) (src >> 32);
+    const uint32_t part = ((lane & 3u) - (lane >> 4)) & 3u;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t w = 16u * i + (lane >> 2);
+      const uint32_t lo = __shfl(slo, (int) w), hi = __shfl(shi, (int) w);
+      const uint64_t a = ((uint64_t) hi << 32) | lo;
+      if (a != ~(uint64_t) 0)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(p.bytes + a + 16u * part),
+                                         (__attribute__((address_space(3))) void *) (db + 1024u * i), 16, 0, 0);
+    }
+#endif
   };
 
   refill_pend();
@@ -395,12 +458,7 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
     const uint64_t p_o0 = pend_o0, p_o1 = pend_o1;
     const uint32_t nw_kind_prev = nw_kind;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the window's LDS-DMA has landed */
-    {
-      const uint8_t *sb = lds + stage + (buf ^ kStageBuf);
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-        W[q] = nw_kind_prev ? *reinterpret_cast<const u32x4 *>(sb + stage_off(lane, q)) : u32x4{0, 0, 0, 0};
-    }
+    read_half(nw_kind_prev, 0);
 #ifdef RHP_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     RHP_STAMP(t1); acc[0] += t1 - t0; t0 = t1;
@@ -438,35 +496,32 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
       nw_ptr = p_o0 & ~(uint64_t) 3;
       nw_kind = 2;
     }
-    {
-      /* the wave fetches all 64 windows with 4 LDS-DMA loads, 16 windows of 64 B each */
-      const uint64_t src = nw_kind ? nw_ptr : ~(uint64_t) 0;
-      const uint32_t slo = (uint32_t) src, shi = (uint32_t) (src >> 32);
-      const uint32_t part = ((lane & 3u) - (lane >> 4)) & 3u;
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const uint32_t w = 16u * i + (lane >> 2);
-        const uint32_t lo = __shfl(slo, (int) w), hi = __shfl(shi, (int) w);
-        const uint64_t a = ((uint64_t) hi << 32) | lo;
-        if (a != ~(uint64_t) 0)
-          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(p.bytes + a + 16u * part),
-                                           (__attribute__((address_space(3))) void *) (lds + stage + buf + 1024u * i),
-                                           16, 0, 0);
-      }
-      buf ^= kStageBuf;
-    }
+    if (!kDoubleStage) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   /* [A]'s reads of this buffer are done */
+    issue_half(0);
+    if (kDoubleStage) buf ^= kStageBuf;
     if (!__ballot(has || nw_kind || pend_ok)) break;
 #ifdef RHP_STAMPS
     RHP_STAMP(t1); acc[3] += t1 - t0; t0 = t1;
 #endif
-    /* 64 steps (idle lanes step in the parked terminal state) */
+    /* kBlock steps (idle lanes step in the parked terminal state) */
     block_pos = pos;
-    ev_lo = 0;
-    ev_hi = 0;
-    steps(W[0], ev_lo, 0);
-    steps(W[1], ev_lo, 16);
-    steps(W[2], ev_hi, 0);
-    steps(W[3], ev_hi, 16);
+#pragma unroll
+    for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
+    steps(W[0], ev[0], 0);
+    steps(W[1], ev[0], 16);
+    steps(W[2], ev[1], 0);
+    steps(W[3], ev[1], 16);
+    if (kHalves == 2) {
+      /* second half of this window, then refill that half with the next window's */
+      __builtin_amdgcn_sched_barrier(0);
+      read_half(nw_kind_prev, 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      issue_half(1);
+      steps(W[0], ev[kEvWords - 2], 0);
+      steps(W[1], ev[kEvWords - 2], 16);
+      steps(W[2], ev[kEvWords - 1], 0);
+      steps(W[3], ev[kEvWords - 1], 16);
+    }
     pos += (int32_t) kBlock;
 #ifdef RHP_STAMPS
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -488,10 +543,10 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
    * registers are live in it.  The wave walks the chunks it took, one request
    * per lane, and finishes what finalize deferred: the exact scalar path, and
    * http_read_request framing of DFA-parsed requests in http mode. */
+#ifndef RHP_NO_REPLAY   /* timing experiment only: deferred requests stay unfinished */
   if (__ballot(deferred)) {
     for (uint32_t k = 0; k < nlist; k++) {
-      const uint32_t c = chunk_list[k];
-      const uint32_t lo = c * p.chunk, hi = min(lo + p.chunk, p.n);
+      const uint32_t lo = chunk_list[k], hi = min(lo + p.chunk, wg_hi);
       for (uint32_t i = lo + lane; i < hi; i += 64) {
         const uint32_t f = p.reqs[i].flags;
         if (!(f & (kDeferExact | kDeferFrame))) continue;
@@ -507,18 +562,8 @@ __global__ __launch_bounds__(WAVES * 64) void rhp_dfa_kernel(Params p)
       }
     }
   }
+#endif
 
-  /* the last workgroup out re-arms the work counters for the next launch, so a
-   * step is exactly one kernel launch (no memset) */
-  __syncthreads();
-  if (tid == 0) {
-    __threadfence();
-    uint32_t done = atomicAdd(&p.work[1], 1u);
-    if (done == gridDim.x - 1) {
-      atomicExch(&p.work[0], 0u);
-      atomicExch(&p.work[1], 0u);
-    }
-  }
 }
 
 /* Exact-path-only kernel: one request per thread, grid-stride (RHP_IMPL_EXACT). */
@@ -539,7 +584,7 @@ int g_cus = 0;
 template <int WAVES>
 int launch_dfa(const Params &prm, hipStream_t s)
 {
-  const size_t lds_bytes = kLdsTable + (size_t) WAVES * (kStageWave + 4 * kChunkCap);
+  const size_t lds_bytes = kLdsTable + (size_t) WAVES * (kStageWave + 4 * kChunkCap) + 16;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES>),
@@ -554,15 +599,17 @@ int launch_dfa(const Params &prm, hipStream_t s)
   uint32_t grid = (uint32_t) (g_cus * per_cu);
   uint32_t need = (prm.n + 64 * WAVES - 1) / (64 * WAVES);
   if (grid > need) grid = need > 0 ? need : 1;
-  /* chunk size: >= 256 requests, and large enough that the pool runs dry before
-   * any wave has used its kChunkCap list entries twice over */
+  /* each workgroup owns n/grid requests; its waves take sub-chunks of >= 64
+   * requests, sized so the range is at most a quarter of what the waves' replay
+   * lists can hold (kChunkCap each), so no wave runs out of list before the
+   * range runs dry */
   Params q = prm;
-  const uint64_t waves = (uint64_t) grid * WAVES;
-  uint64_t chunk = (2ull * prm.n + waves * kChunkCap - 1) / (waves * kChunkCap);
-  chunk = (chunk + 63) & ~63ull;
-  uint64_t floor_chunk = kPoolChunk;
-  if (const char *e = getenv("RHP_CHUNK")) floor_chunk = (uint64_t) atoi(e);   /* experiments */
-  q.chunk = (uint32_t) (chunk < floor_chunk ? floor_chunk : chunk);
+  q.span = (prm.n + grid - 1) / grid;
+  uint32_t sub = (q.span + WAVES * kChunkCap / 4 - 1) / (WAVES * kChunkCap / 4);
+  uint32_t floor_sub = 64;
+  if (const char *e = getenv("RHP_CHUNK")) floor_sub = (uint32_t) atoi(e);   /* experiments */
+  sub = (sub + 63) & ~63u;
+  q.chunk = sub < floor_sub ? floor_sub : sub;
   hipLaunchKernelGGL(rhp_dfa_kernel<WAVES>, dim3(grid), dim3(WAVES * 64), lds_bytes, s, q);
   return (int) hipGetLastError();
 }
@@ -629,6 +676,7 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.max_headers = b->max_headers;
   prm.mode = b->mode;
   prm.chunk = kPoolChunk;
+  prm.span = 0;
   {
     const char *e = getenv("RHP_EXPERIMENT");   /* timing experiments only: breaks results */
     prm.pad = e ? (uint32_t) atoi(e) : 0u;
@@ -644,6 +692,8 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   case 4: return launch_dfa<4>(prm, s);
   case 8: return launch_dfa<8>(prm, s);
   case 11: return launch_dfa<11>(prm, s);
+  case 10: return launch_dfa<10>(prm, s);
+  case 12: return launch_dfa<12>(prm, s);
   default: return launch_dfa<16>(prm, s);
   }
 }

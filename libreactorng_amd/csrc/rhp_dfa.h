@@ -46,6 +46,12 @@
 #define RHP_DHD
 #endif
 
+/* bytes of a lane's window per kernel loop iteration: the DFA steps this many
+ * bytes between two decodes (kernel and emulator must agree) */
+#ifndef RHP_BLOCK
+#define RHP_BLOCK 64
+#endif
+
 namespace rhp {
 
 enum State : uint32_t {

@@ -69,35 +69,44 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
     dec_reset(d);
     rhp_hdr_t *hout = b->hdrs + (uint64_t) i * maxh;
     for (;;) {
-      /* one 64-byte block: steps, then the decode of its event mask */
+      /* one RHP_BLOCK-byte block: steps, then the decode of its event mask */
       const int32_t block_pos = pos;
-      uint64_t ev = 0;
-      for (int k = 0; k < 64; k++) {
-        st = T.w[(st >> 1) + win[k]];
-        ev |= (uint64_t) event_of(st) << k;
+      uint64_t evw[RHP_BLOCK / 64];
+      for (int w = 0; w < RHP_BLOCK / 64; w++) {
+        uint64_t ev = 0;
+        for (int k = 0; k < 64; k++) {
+          st = T.w[(st >> 1) + win[64 * w + k]];
+          ev |= (uint64_t) event_of(st) << k;
+        }
+        evw[w] = ev;
       }
-      win += 64;
-      pos += 64;
+      win += RHP_BLOCK;
+      pos += RHP_BLOCK;
       const bool slow = st == row_of(S_SLOW);
       const bool term_ev = is_done_row(st) || is_err_row(st);
-      uint64_t m = slow ? 0 : ev;
       uint32_t term_pos = 0xffffffffu;
-      while (m) {
-        const uint32_t bit = (uint32_t) __builtin_ctzll(m);
-        m &= m - 1;
-        const uint32_t ep = (uint32_t) (block_pos + (int32_t) bit);
-        if (term_ev && m == 0) {
-          term_pos = ep;
-        } else {
+      if (term_ev) {   /* the terminal is the block's last event */
+        for (int w = RHP_BLOCK / 64 - 1; w >= 0; w--)
+          if (evw[w]) {
+            const uint32_t bt = 63u - (uint32_t) __builtin_clzll(evw[w]);
+            term_pos = (uint32_t) (block_pos + 64 * w) + bt;
+            evw[w] &= ~(1ull << bt);
+            break;
+          }
+      }
+      for (int w = 0; w < RHP_BLOCK / 64 && !slow; w++) {
+        uint64_t m = evw[w];
+        while (m && !d.ovf) {
+          const uint32_t bit = (uint32_t) __builtin_ctzll(m);
+          m &= m - 1;
           uint32_t lo, hi;
-          if (dec_event(d, ep, maxh, lo, hi)) {
+          if (dec_event(d, (uint32_t) (block_pos + 64 * w) + bit, maxh, lo, hi)) {
             rhp_hdr_t &o = hout[d.nh - 1];
             o.name_off = (uint16_t) lo;
             o.name_len = (uint16_t) (lo >> 16);
             o.value_off = (uint16_t) hi;
             o.value_len = (uint16_t) (hi >> 16);
           }
-          if (d.ovf) m = 0;
         }
       }
       const bool ovf = d.ovf != 0;

@@ -49,13 +49,9 @@ struct Params {
   uint32_t max_headers;
   uint32_t mode;
   uint32_t pad;
-  uint32_t chunk;   /* requests per sub-chunk a wave takes */
   uint32_t span;    /* requests per workgroup */
 };
 
-#ifndef RHP_BLOCK
-#define RHP_BLOCK 64
-#endif
 #ifndef RHP_SINGLE_STAGE
 #define RHP_SINGLE_STAGE 0
 #endif
@@ -63,7 +59,6 @@ struct Params {
 #define RHP_MIN_WAVES_PER_SIMD 1
 #endif
 enum : uint32_t {
-  kPoolChunk = 256,
   kBlock = RHP_BLOCK,                            /* window bytes per lane per loop iteration */
   kHalves = kBlock / 64,                         /* 64-byte halves per window */
   kEvWords = kBlock / 32,
@@ -71,7 +66,6 @@ enum : uint32_t {
   kStageBuf = 64 * kBlock,                       /* one window per lane */
   kDoubleStage = kHalves == 1 && !RHP_SINGLE_STAGE,
   kStageWave = kDoubleStage ? 2 * kStageBuf : kStageBuf,   /* double-buffered, or refilled right after it is read */
-  kChunkCap = 32,                                /* chunks one wave may take (its replay list) */
   kDeferExact = 0x8000u,                         /* reqs[i].flags while deferred (kernel-internal) */
   kDeferFrame = 0x4000u
 };
@@ -213,7 +207,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_ke
     const u32x4 *src = reinterpret_cast<const u32x4 *>(&g_table);
     u32x4 *dst = reinterpret_cast<u32x4 *>(lds);
     for (uint32_t k = tid; k < kTableBytes / 16; k += WAVES * 64) dst[k] = src[k];
-    if (tid == 0) *reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * (kStageWave + 4 * kChunkCap)) = 0;
+    if (tid < 2) reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave)[tid] = 0;   /* pool counter, replay flag */
   }
   __syncthreads();
 
@@ -244,48 +238,34 @@ __global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_ke
   uint32_t buf = 0;                    /* buffer the next window lands in */
 
   /* ---- request pool ----
-   * Workgroup g owns requests [g*span, (g+1)*span) (host: span = n / grid); its
-   * waves pull sub-chunks of p.chunk requests from an LDS counter, so the waves
-   * of a CU balance among themselves and no global atomic is ever touched.
-   * Each wave records its sub-chunks (at most kChunkCap; the host sizes p.chunk
-   * so the workgroup's range fits 16x over) for the post-loop replay. */
+   * Workgroup g owns requests [g*span, (g+1)*span) (host: span = n / grid).
+   * Lanes that need their next request take it from the workgroup's LDS
+   * counter (one atomic per wave and refill, for all of the wave's lanes that
+   * need one), so the 16 waves of a CU drain one shared range request by
+   * request and finish together; no global atomic is ever touched. */
   const uint32_t wg_lo = min(blockIdx.x * p.span, p.n), wg_hi = min(wg_lo + p.span, p.n);
-  uint32_t *chunk_list = reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave) + (tid >> 6) * kChunkCap;
-  uint32_t *wg_counter = reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * (kStageWave + 4 * kChunkCap));
-  uint32_t nlist = 0;                  /* wave-uniform */
-  bool deferred = false;               /* this lane left requests for the replay */
-  uint32_t pool_next = 0, pool_end = 0;
-  bool pool_dry = false;
+  uint32_t *wg_counter = reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave);
+  uint32_t *wg_deferred = wg_counter + 1;   /* some request of the range needs the replay */
+  bool pool_dry = wg_lo >= wg_hi;
 
   /* give every lane without a pending request one from the pool; the offsets
    * loads are only consumed at the top of the next block */
   auto refill_pend = [&]() {
-    uint64_t want = __ballot(!pend_ok);
-    while (want && !pool_dry) {
-      if (pool_next >= pool_end) {
-        if (nlist == kChunkCap) { pool_dry = true; break; }
-        uint32_t c = 0;
-        if (lane == 0) c = atomicAdd(wg_counter, 1u);
-        c = __builtin_amdgcn_readfirstlane(c);
-        const uint32_t lo = wg_lo + c * p.chunk;
-        if (c >= (wg_hi - wg_lo + p.chunk - 1) / p.chunk) { pool_dry = true; break; }
-        if (lane == 0) chunk_list[nlist] = lo;
-        nlist++;
-        pool_next = lo;
-        pool_end = min(lo + p.chunk, wg_hi);
-      }
-      uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
-      uint32_t avail = pool_end - pool_next;
-      if (!pend_ok && rank < avail) {
-        pend = pool_next + rank;
-        typedef uint64_t u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
-        const u64x2a8 o = *GLOBAL(const u64x2a8, p.offsets + pend);   /* offsets[pend], offsets[pend+1] */
-        pend_o0 = o[0];
-        pend_o1 = o[1];
-        pend_ok = true;
-      }
-      pool_next += min((uint32_t) __popcll(want), avail);
-      want = __ballot(!pend_ok);
+    const uint64_t want = __ballot(!pend_ok);
+    if (!want || pool_dry) return;
+    const uint32_t cnt = (uint32_t) __popcll(want);
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(wg_counter, cnt);
+    base = wg_lo + __builtin_amdgcn_readfirstlane(base);
+    if (base + cnt >= wg_hi) pool_dry = true;
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
+    if (!pend_ok && base + rank < wg_hi) {
+      pend = base + rank;
+      typedef uint64_t u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
+      const u64x2a8 o = *GLOBAL(const u64x2a8, p.offsets + pend);   /* offsets[pend], offsets[pend+1] */
+      pend_o0 = o[0];
+      pend_o1 = o[1];
+      pend_ok = true;
     }
   };
 
@@ -376,13 +356,13 @@ __global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_ke
       r.minor_version = (int8_t) (d.rl23 >> 16);
       r.num_headers = (uint16_t) d.nh;
       r.flags = p.mode == RHP_MODE_HTTP ? (uint16_t) kDeferFrame : (uint16_t) 0;   /* framing: replay */
-      deferred |= p.mode == RHP_MODE_HTTP;
+      if (p.mode == RHP_MODE_HTTP) *wg_deferred = 1u;
     } else if (bad) {
       r.ret = -1;
       if (p.mode == RHP_MODE_HTTP) store_http_bad(p.http + cur);
     } else {
       r.flags = (uint16_t) kDeferExact;   /* exact path: replay */
-      deferred = true;
+      *wg_deferred = 1u;
     }
     if (!(p.pad & 2)) store_req(p.reqs + cur, r);
     has = false;
@@ -540,30 +520,28 @@ __global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_ke
 #endif
 
   /* Replay: the rare paths run here, after the DFA loop, so none of their
-   * registers are live in it.  The wave walks the chunks it took, one request
-   * per lane, and finishes what finalize deferred: the exact scalar path, and
-   * http_read_request framing of DFA-parsed requests in http mode. */
+   * registers are live in it.  Once every wave of the workgroup is done, the
+   * workgroup walks its range, one request per thread, and finishes what
+   * finalize deferred: the exact scalar path, and http_read_request framing of
+   * DFA-parsed requests in http mode.  Nothing to do -> no pass at all. */
 #ifndef RHP_NO_REPLAY   /* timing experiment only: deferred requests stay unfinished */
-  if (__ballot(deferred)) {
-    for (uint32_t k = 0; k < nlist; k++) {
-      const uint32_t lo = chunk_list[k], hi = min(lo + p.chunk, wg_hi);
-      for (uint32_t i = lo + lane; i < hi; i += 64) {
-        const uint32_t f = p.reqs[i].flags;
-        if (!(f & (kDeferExact | kDeferFrame))) continue;
-        const uint64_t off = p.offsets[i], len = p.offsets[i + 1] - off;
-        if (f & kDeferExact) {
-          finish_exact(p, i, off, len);
-        } else {
-          rhp_req_t r = p.reqs[i];
-          r.flags = 0;
-          finish_http(p, i, off, len, r);
-          p.reqs[i].flags = 0;
-        }
+  __syncthreads();
+  if (*wg_deferred) {
+    for (uint32_t i = wg_lo + tid; i < wg_hi; i += WAVES * 64) {
+      const uint32_t f = p.reqs[i].flags;
+      if (!(f & (kDeferExact | kDeferFrame))) continue;
+      const uint64_t off = p.offsets[i], len = p.offsets[i + 1] - off;
+      if (f & kDeferExact) {
+        finish_exact(p, i, off, len);
+      } else {
+        rhp_req_t r = p.reqs[i];
+        r.flags = 0;
+        finish_http(p, i, off, len, r);
+        p.reqs[i].flags = 0;
       }
     }
   }
 #endif
-
 }
 
 /* Exact-path-only kernel: one request per thread, grid-stride (RHP_IMPL_EXACT). */
@@ -584,7 +562,7 @@ int g_cus = 0;
 template <int WAVES>
 int launch_dfa(const Params &prm, hipStream_t s)
 {
-  const size_t lds_bytes = kLdsTable + (size_t) WAVES * (kStageWave + 4 * kChunkCap) + 16;
+  const size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + 16;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES>),
@@ -599,17 +577,9 @@ int launch_dfa(const Params &prm, hipStream_t s)
   uint32_t grid = (uint32_t) (g_cus * per_cu);
   uint32_t need = (prm.n + 64 * WAVES - 1) / (64 * WAVES);
   if (grid > need) grid = need > 0 ? need : 1;
-  /* each workgroup owns n/grid requests; its waves take sub-chunks of >= 64
-   * requests, sized so the range is at most a quarter of what the waves' replay
-   * lists can hold (kChunkCap each), so no wave runs out of list before the
-   * range runs dry */
+  /* each workgroup owns a contiguous n/grid share of the requests */
   Params q = prm;
   q.span = (prm.n + grid - 1) / grid;
-  uint32_t sub = (q.span + WAVES * kChunkCap / 4 - 1) / (WAVES * kChunkCap / 4);
-  uint32_t floor_sub = 64;
-  if (const char *e = getenv("RHP_CHUNK")) floor_sub = (uint32_t) atoi(e);   /* experiments */
-  sub = (sub + 63) & ~63u;
-  q.chunk = sub < floor_sub ? floor_sub : sub;
   hipLaunchKernelGGL(rhp_dfa_kernel<WAVES>, dim3(grid), dim3(WAVES * 64), lds_bytes, s, q);
   return (int) hipGetLastError();
 }
@@ -675,7 +645,6 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.n = b->n;
   prm.max_headers = b->max_headers;
   prm.mode = b->mode;
-  prm.chunk = kPoolChunk;
   prm.span = 0;
   {
     const char *e = getenv("RHP_EXPERIMENT");   /* timing experiments only: breaks results */

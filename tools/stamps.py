@@ -7,7 +7,7 @@ time of the same launch, i.e. the shader clock the kernel actually ran at.
 import ctypes, os, sys
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["RHP_LIB"] = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libreactorng_amd", "librhp_stamps.so")
+os.environ["RHP_LIB"] = os.environ.get("RHP_STAMPS_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libreactorng_amd", "librhp_stamps.so"))
 import torch
 import libreactorng_amd as rhp
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else rhp.GEN_GET256
@@ -41,3 +41,18 @@ for k in range(5):
 pre, whole = f[used, 6], f[used, 7]
 print(f"  launch {ms * 1e3:.1f} us (HIP events); per wave: entry->loop {pre.mean():.0f}, entry->exit mean {whole.mean():.0f}"
       f" max {whole.max():.0f}, loop sections {tot.sum() / used.sum():.0f} (memtime ticks)")
+# per-workgroup spread (waves g*W..g*W+W-1 form workgroup g; XCD = g % 8 under round-robin dispatch)
+W = int(os.environ.get("RHP_WAVES", "16"))
+ng = used.sum() // W
+if ng:
+    wg = whole[: ng * W].reshape(ng, W).max(axis=1)
+    print(f"  per-workgroup entry->exit: min {wg.min():.0f} mean {wg.mean():.0f} max {wg.max():.0f}")
+    xcd = np.array([wg[np.arange(ng) % 8 == x].mean() for x in range(8)])
+    print("  mean per XCD (g % 8): " + " ".join(f"{v:.0f}" for v in xcd))
+    slow = np.argsort(wg)[-8:]
+    print("  slowest workgroups: " + " ".join(str(int(g)) for g in slow))
+if ng:
+    per_idx = whole[: ng * W].reshape(ng, W)
+    print("  mean entry->exit by wave index in workgroup: " + " ".join(f"{v / 1000:.0f}k" for v in per_idx.mean(axis=0)))
+    its = f[used, 5][: ng * W].reshape(ng, W)
+    print("  mean iterations by wave index: " + " ".join(f"{v:.1f}" for v in its.mean(axis=0)))

@@ -3,14 +3,19 @@
  * and the event decoder that turns its output into phr_parse_request records.
  *
  * The table re-expresses phr_parse_request (picohttpparser.c:341-409, headers
- * :263-339) as u16 entries over (state, byte): an entry is the LDS byte offset
- * of the next state's row, so one step is  e = T[e + 2*byte]  (one ds_read_u16).
+ * :263-339) as u8 entries over (state, byte).  State s has the index idx8(s)
+ * and its row of 256 next-state indices lives at LDS byte idx8(s) * 256, so a
+ * step is
  *
- * Events.  Rows live in two LDS ranges: plain rows below kEventRow and event
- * rows at/above it, so bit 14 of an entry says "this transition is an event".
- * The kernel ORs that bit into a per-block mask (two VALU ops per step, no LDS
- * write) and decodes the mask once per block.  For a request the fast path
- * accepts, the event sequence is fixed by the grammar:
+ *     a = v_perm(state, window dword, sel)   = state * 256 + byte
+ *     state = T8[a]                          one ds_read_u8
+ *     ev = v_alignbit(state, ev, 1)          bit 0 of the index -> event mask
+ *
+ * Events.  Plain states have even indices and event states odd ones, so bit 0
+ * of an index says "the transition that entered this state is an event"; the
+ * kernel shifts that bit into a per-lane 32-bit mask with one VALU op and
+ * decodes the mask once per block.  For a request the fast path accepts, the
+ * event sequence is fixed by the grammar:
  *
  *   ME  PE  RL              request line: method end (the SP; the path starts
  *                           right after it), path end (the next SP), RL = the
@@ -74,26 +79,24 @@ enum State : uint32_t {
 };
 
 enum : uint32_t {
-  kRowBytes = 528,             /* 256 u16 entries + 16 pad: rows rotate LDS banks by 4 */
-  kEventBit = 14,
-  kEventRow = 1u << kEventBit, /* first event row */
-  kTableBytes = kEventRow + (S_COUNT - S_NUM_PLAIN) * kRowBytes,
   kFastMaxLen = 65535 - 256    /* longer requests take the exact path (u16 positions) */
 };
-static_assert(S_NUM_PLAIN * kRowBytes <= kEventRow, "plain rows must fit below the event rows");
-static_assert(kTableBytes + 2 * 256 < 32768, "entries stay below bit 15");
 
-constexpr uint32_t row_of(uint32_t s)
+/* u8 index of a state: plain states even, event states odd */
+RHP_DHD constexpr uint32_t idx8(uint32_t s)
 {
-  return s < S_NUM_PLAIN ? s * kRowBytes : kEventRow + (s - S_NUM_PLAIN) * kRowBytes;
+  return s < S_NUM_PLAIN ? 2u * s : 2u * (s - S_NUM_PLAIN) + 1u;
 }
-RHP_DHD constexpr bool is_terminal_row(uint32_t row)
-{
-  return row < row_of(S_SKIP3) || (row >= row_of(S_DONE_E) && row < row_of(S_SP1_E));
-}
-RHP_DHD constexpr bool is_done_row(uint32_t row) { return row == row_of(S_DONE) || row == row_of(S_DONE_E); }
-RHP_DHD constexpr bool is_err_row(uint32_t row) { return row == row_of(S_ERR) || row == row_of(S_ERR_E); }
-RHP_DHD constexpr uint32_t event_of(uint32_t row) { return row >> kEventBit; }
+enum : uint32_t {
+  kRows8 = 2u * (S_NUM_PLAIN - 1u) + 1u,   /* highest index + 1 (the last plain state) */
+  kTable8Bytes = kRows8 * 256u
+};
+static_assert(2u * (S_COUNT - S_NUM_PLAIN) - 1u < kRows8, "event indices fit below the last plain row");
+static_assert(kRows8 <= 256u, "indices are bytes");
+
+RHP_DHD constexpr bool is_done8(uint32_t e) { return e == idx8(S_DONE) || e == idx8(S_DONE_E); }
+RHP_DHD constexpr bool is_err8(uint32_t e) { return e == idx8(S_ERR) || e == idx8(S_ERR_E); }
+RHP_DHD constexpr bool is_slow8(uint32_t e) { return e == idx8(S_SLOW); }
 
 constexpr bool c_tchar(uint32_t c)
 {
@@ -177,16 +180,16 @@ constexpr uint32_t step(uint32_t s, uint32_t c)
   }
 }
 
-struct Table {
-  uint16_t w[kTableBytes / 2];
+struct Table8 {
+  uint8_t b[kTable8Bytes];
 };
 
-constexpr Table make_table()
+constexpr Table8 make_table8()
 {
-  Table t{};
-  for (uint32_t i = 0; i < kTableBytes / 2; i++) t.w[i] = (uint16_t) row_of(S_SLOW);
+  Table8 t{};
+  for (uint32_t i = 0; i < kTable8Bytes; i++) t.b[i] = (uint8_t) idx8(S_SLOW);   /* unused rows */
   for (uint32_t s = 0; s < S_COUNT; s++)
-    for (uint32_t c = 0; c < 256; c++) t.w[(row_of(s) >> 1) + c] = (uint16_t) row_of(step(s, c));
+    for (uint32_t c = 0; c < 256; c++) t.b[idx8(s) * 256u + c] = (uint8_t) idx8(step(s, c));
   return t;
 }
 

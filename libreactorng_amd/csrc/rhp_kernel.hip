@@ -6,19 +6,24 @@
  * HBM.  Design:
  *
  *  - one request per lane, 64 requests per wave in flight; every lane runs the
- *    byte DFA of rhp_dfa.h in lockstep: per byte one ds_read_u16 of the table in
- *    LDS and two VALU ops that OR the entry's event bit into a 64-bit block
- *    mask -- no LDS write and no divergence on the byte path;
- *  - lanes stream their request in 64-byte windows (4 x global_load_dwordx4 at
- *    4-byte alignment; unaligned starts enter through SKIP states), the next
- *    window issued a whole block ahead; every lane also holds its NEXT
- *    request's offsets, so a request switch never waits on a dependent load;
+ *    byte DFA of rhp_dfa.h in lockstep.  One step is one LDS read and two VALU:
+ *        a     = v_perm(state, window dword, sel)   = state * 256 + byte
+ *        state = T8[a]                               ds_read_u8, next index
+ *        ev    = v_alignbit(state, ev, 1)            odd index = event bit
+ *    no LDS write and no divergence on the byte path;
+ *  - a step waits on its own LDS read (a dependent chain per lane), so the
+ *    throughput comes from waves in flight: the lane state is kept small
+ *    (<= 64 VGPRs: 8 waves per SIMD) and the window staging single-buffered
+ *    (4 KiB per wave: two 16-wave workgroups per CU);
+ *  - lanes stream their request in 64-byte windows: the wave fetches its 64
+ *    lanes' next windows with four LDS-DMA loads (16 windows x 64 B each), a
+ *    whole block ahead of use; every lane also holds its NEXT request's
+ *    offsets, so a request switch never waits on a dependent load;
  *  - once per block the event mask is decoded (rhp_dfa.h dec_event) into the
- *    request-line record and header records, which are stored to HBM in
- *    16-byte pairs; finished requests are finalized and new ones handed out
- *    (persistent waves pull 256-request chunks from one atomic counter);
- *  - a request whose outcome depends on where its buffer ends, or that takes a
- *    rare path (S_SLOW), is finished by the exact scalar path (rhp_scalar.h).
+ *    request-line record and header records (stored in 16-byte pairs);
+ *  - a request the table cannot decide alone (S_SLOW, a terminal at/after
+ *    len, no terminal by the end of its buffer) and http framing are finished
+ *    after the loop by the exact scalar path (rhp_scalar.h).
  *
  * The algorithm is mirrored block for block by rhp_emu.cpp (CPU tests).
  */
@@ -35,7 +40,7 @@ namespace {
 
 using namespace rhp;
 
-__device__ const Table g_table = make_table();
+__device__ const Table8 g_table8 = make_table8();
 
 struct Params {
   const uint8_t *bytes;
@@ -48,45 +53,54 @@ struct Params {
   uint32_t n;
   uint32_t max_headers;
   uint32_t mode;
-  uint32_t pad;
   uint32_t span;    /* requests per workgroup */
 };
 
-#ifndef RHP_SINGLE_STAGE
-#define RHP_SINGLE_STAGE 0
+#ifndef RHP_WAVES_PER_SIMD
+#define RHP_WAVES_PER_SIMD 8
 #endif
-#ifndef RHP_MIN_WAVES_PER_SIMD
-#define RHP_MIN_WAVES_PER_SIMD 1
-#endif
+
 enum : uint32_t {
-  kBlock = RHP_BLOCK,                            /* window bytes per lane per loop iteration */
-  kHalves = kBlock / 64,                         /* 64-byte halves per window */
-  kEvWords = kBlock / 32,
-  kLdsTable = (kTableBytes + 1023u) & ~1023u,   /* staging starts 1 KiB aligned */
-  kStageBuf = 64 * kBlock,                       /* one window per lane */
-  kDoubleStage = kHalves == 1 && !RHP_SINGLE_STAGE,
-  kStageWave = kDoubleStage ? 2 * kStageBuf : kStageBuf,   /* double-buffered, or refilled right after it is read */
+  kBlock = RHP_BLOCK,                            /* window bytes per lane per loop iteration (64 or 128) */
+  kParts = kBlock / 16,                          /* 16-byte parts per window */
+  kEvWords = kBlock / 32,                        /* 32-bit event words per block */
+  kLdsTable = (kTable8Bytes + 1023u) & ~1023u,  /* staging starts 1 KiB aligned */
+  kStageWave = 64 * kBlock,                      /* one window per lane, single-buffered */
+  kPark = 0,                                     /* idx8(S_DONE): idle lanes step here */
   kDeferExact = 0x8000u,                         /* reqs[i].flags while deferred (kernel-internal) */
   kDeferFrame = 0x4000u
 };
+static_assert(kBlock == 64 || kBlock == 128, "64- or 128-byte windows");
+static_assert(idx8(S_DONE) == kPark, "parked lanes sit in DONE");
 
-/* LDS byte address of part q (16 B) of lane w's window inside one staging
+/* LDS byte address of part q (16 B) of lane w's window inside the staging
  * buffer.  The LDS-DMA loads of a wave write lane-linearly (1 KiB per
- * instruction), so the swizzle lives on the source side: instruction i, lane j
- * fetches part ((j & 3) - (j >> 4)) & 3 of lane 16i + (j >> 2)'s window, which
- * makes each lane's four ds_read_b128 of its own window bank-conflict free. */
+ * instruction), so the swizzle lives on the source side, chosen so that each
+ * lane's ds_read_b128 of its own window are bank-conflict free:
+ *   64-B windows:  instruction i, lane j fetches part ((j & 3) - (j >> 4)) & 3
+ *                  of lane 16i + (j >> 2)'s window (16 windows per load);
+ *   128-B windows: instruction i, lane j fetches part ((j & 7) - (w >> 1)) & 7
+ *                  of lane w = 8i + (j >> 3)'s window (8 whole 128-B lines per
+ *                  load, so every HBM line is fetched by one instruction). */
 __device__ __forceinline__ uint32_t stage_off(uint32_t w, uint32_t q)
 {
-#ifdef RHP_OWN_WINDOW
-  return q * 1024u + w * 16u;
-#endif
-  const uint32_t u = w & 15u;
-  return (q >> 2) * 4096u + (w >> 4) * 1024u + u * 64u + ((q + (u >> 2)) & 3u) * 16u;
+  if (kBlock == 64) {
+    const uint32_t u = w & 15u;
+    return (w >> 4) * 1024u + u * 64u + ((q + (u >> 2)) & 3u) * 16u;
+  }
+  return (w >> 3) * 1024u + (w & 7u) * 128u + ((q + (w >> 1)) & 7u) * 16u;
+}
+__device__ __forceinline__ uint32_t dma_window(uint32_t i, uint32_t j)   /* whose window lane j fetches in load i */
+{
+  return kBlock == 64 ? 16u * i + (j >> 2) : 8u * i + (j >> 3);
+}
+__device__ __forceinline__ uint32_t dma_part(uint32_t w, uint32_t j)     /* ... and which 16-byte part of it */
+{
+  return kBlock == 64 ? ((j & 3u) - (j >> 4)) & 3u : ((j & 7u) - (w >> 1)) & 7u;
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
 
 #ifdef RHP_STAMPS
 /* diagnostic build only: per-wave cycle sums per loop section (never read by the kernel) */
@@ -98,22 +112,10 @@ __device__ unsigned long long g_stamps[8192 * 8];
 #define RHP_STAMP(t) do { } while (0)
 #endif
 
-/* 16 bytes at a 4-byte aligned global address */
-__device__ __forceinline__ u32x4 load_chunk(const uint8_t *p)
-{
-  typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-  return *reinterpret_cast<const u32x4a4 *>(p);
-}
-
 /* Exact scalar path for one request (phr or http mode).  Only called from the
- * post-loop replay, where inlining it lets it reuse the loop's dead registers
- * (a call there costs ~14 VGPRs of calling-convention overhead). */
+ * post-loop replay, where inlining it lets it reuse the loop's dead registers. */
 __device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64_t off, uint64_t len)
 {
-#ifdef RHP_EXPERIMENT_NO_EXACT
-  p.reqs[i].ret = -9;
-  return;
-#endif
   rhp_req_t r;
   r.flags = RHP_F_EXACT;
   rhp_hdr_t *h = p.hdrs + (uint64_t) i * p.max_headers;
@@ -149,13 +151,13 @@ __device__ __forceinline__ void finish_http(const Params &p, uint32_t i, uint64_
  * global_store (VM counter only), not flat_store (VM + LGKM). */
 #define GLOBAL(T, x) ((__attribute__((address_space(1))) T *) (x))
 
-/* ev |= event bit of entry st at bit position `bit`.  Written as asm so the
- * compiler cannot reassociate a block's ORs into one tree at its end, which
- * would keep every step's entry alive in its own VGPR. */
-__device__ __forceinline__ void ev_or(uint32_t &ev, uint32_t st, uint32_t bit)
+/* ev = (ev >> 1) | (st << 31): bit 0 of the state index (the event bit) into
+ * the top of the mask.  Written as asm so the compiler cannot sink the shifts
+ * of a block's steps into one chain at its end, which would keep every step's
+ * state alive in its own VGPR. */
+__device__ __forceinline__ void ev_shift(uint32_t &ev, uint32_t st)
 {
-  uint32_t t;
-  asm("v_lshrrev_b32 %1, 14, %2\n\tv_lshl_or_b32 %0, %1, %3, %0" : "+v"(ev), "=&v"(t) : "v"(st), "s"(bit));
+  asm("v_alignbit_b32 %0, %1, %0, 1" : "+v"(ev) : "v"(st));
 }
 
 /* a 16-byte header-record pair, or a single record, at 4-byte alignment */
@@ -192,7 +194,7 @@ __device__ __forceinline__ void store_http_bad(rhp_http_t *dst)
  * table.  Persistent: grid = workgroups resident on the device.
  */
 template <int WAVES>
-__global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_kernel(Params p)
+__global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel(Params p)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid = threadIdx.x;
@@ -204,49 +206,57 @@ __global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_ke
 #endif
 
   {
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(&g_table);
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(&g_table8);
     u32x4 *dst = reinterpret_cast<u32x4 *>(lds);
-    for (uint32_t k = tid; k < kTableBytes / 16; k += WAVES * 64) dst[k] = src[k];
+    for (uint32_t k = tid; k < kTable8Bytes / 16; k += WAVES * 64) dst[k] = src[k];
     if (tid < 2) reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave)[tid] = 0;   /* pool counter, replay flag */
   }
   __syncthreads();
 
   const uint32_t maxh = p.max_headers;
-  const uint32_t park = row_of(S_DONE);
-
-  /* ---- lane state ---- */
-  uint32_t st = park;                  /* LDS offset of the current state's row (= the last entry) */
-  int32_t pos = 0, block_pos = 0;      /* request-relative position of the next byte / of the block */
-  uint32_t ev[kEvWords];               /* events of the block just stepped */
-#pragma unroll
-  for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
-  bool has = false;                    /* cur is being parsed */
-  uint32_t cur = 0, cur_len = 0;
-  uint64_t cur_off = 0, cur_ptr = 0;   /* cur_ptr: byte offset of the window in W */
-  Dec d;
-  dec_reset(d);
-  uint32_t rec_lo = 0, rec_hi = 0;     /* header record waiting for its pair */
-  bool pend_ok = false;                /* pend: the lane's next request */
-  uint32_t pend = 0;
-  uint64_t pend_o0 = 0, pend_o1 = 0;   /* offsets[pend], offsets[pend+1] as loaded */
-  uint32_t nw_kind = 0;                /* next window: 0 none, 1 continuation, 2 first window of pend */
-  uint64_t nw_ptr = 0;
-  u32x4 W[4];
-#pragma unroll
-  for (int q = 0; q < 4; q++) W[q] = u32x4{0, 0, 0, 0};
-  const uint32_t stage = kLdsTable + (tid >> 6) * kStageWave;   /* this wave's two buffers */
-  uint32_t buf = 0;                    /* buffer the next window lands in */
 
   /* ---- request pool ----
    * Workgroup g owns requests [g*span, (g+1)*span) (host: span = n / grid).
    * Lanes that need their next request take it from the workgroup's LDS
    * counter (one atomic per wave and refill, for all of the wave's lanes that
-   * need one), so the 16 waves of a CU drain one shared range request by
-   * request and finish together; no global atomic is ever touched. */
+   * need one), so the waves of a workgroup drain one shared range request by
+   * request and finish together; no global atomic is ever touched.
+   * Window addresses are u32 byte offsets from `base` (the 4-aligned start of
+   * the range; the host keeps a batch below 4 GiB). */
   const uint32_t wg_lo = min(blockIdx.x * p.span, p.n), wg_hi = min(wg_lo + p.span, p.n);
   uint32_t *wg_counter = reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave);
   uint32_t *wg_deferred = wg_counter + 1;   /* some request of the range needs the replay */
   bool pool_dry = wg_lo >= wg_hi;
+  const uint64_t base = pool_dry ? 0 : (p.offsets[wg_lo] & ~(uint64_t) 3);
+  const uint8_t *wbytes = p.bytes + base;
+
+  /* ---- lane state ---- */
+  uint32_t st = kPark;                 /* u8 state index */
+  int32_t pos = 0;                     /* request-relative position of the next byte to step */
+  uint32_t ev[kEvWords];               /* events of the block just stepped (32 bytes per word) */
+#pragma unroll
+  for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
+  bool has = false;                    /* cur is being parsed */
+  uint32_t cur = 0, cur_len = 0, cur_ptr = 0;   /* cur_ptr: window of the block being stepped */
+  /* event decoder state of cur (rhp_dfa.h Dec, packed into four registers):
+   *   h01 = e0 | e1 << 16     the two newest event positions
+   *   hx  = e2 | ovf << 16    the third; ovf = 0, or 1 + the line start at
+   *                           which max_headers overflowed
+   *   kn  = k | minor << 3 | nh << 8   events consumed (0..2 request line,
+   *                           then 3,4 = CO, EOL), minor version, headers done
+   *   rl  = method_len | path_len << 16 */
+  uint32_t h01 = 0, hx = 0, kn = 0, rl = 0;
+  uint32_t rec_lo = 0, rec_hi = 0;     /* header record waiting for its pair */
+  bool pend_ok = false;                /* pend: the lane's next request */
+  uint32_t pend = 0;
+  uint32_t pend_o0 = 0, pend_o1 = 0;   /* low dwords of offsets[pend], offsets[pend+1] as loaded */
+  uint32_t nw = 0;                     /* next window: byte offset from base | kind (0 none, 1
+                                          continuation, 2 first window of pend); windows are 4-aligned */
+  /* the window in registers: half of a 64-B window (the other half is read
+   * midway), or a whole 128-B window */
+  constexpr int kWRegs = kBlock == 64 ? 2 : 8;
+  u32x4 W[kWRegs];
+  const uint32_t stage = kLdsTable + (tid >> 6) * kStageWave;
 
   /* give every lane without a pending request one from the pool; the offsets
    * loads are only consumed at the top of the next block */
@@ -254,17 +264,18 @@ __global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_ke
     const uint64_t want = __ballot(!pend_ok);
     if (!want || pool_dry) return;
     const uint32_t cnt = (uint32_t) __popcll(want);
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(wg_counter, cnt);
-    base = wg_lo + __builtin_amdgcn_readfirstlane(base);
-    if (base + cnt >= wg_hi) pool_dry = true;
+    uint32_t b0 = 0;
+    if (lane == 0) b0 = atomicAdd(wg_counter, cnt);
+    b0 = wg_lo + __builtin_amdgcn_readfirstlane(b0);
+    if (b0 + cnt >= wg_hi) pool_dry = true;
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
-    if (!pend_ok && base + rank < wg_hi) {
-      pend = base + rank;
-      typedef uint64_t u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
-      const u64x2a8 o = *GLOBAL(const u64x2a8, p.offsets + pend);   /* offsets[pend], offsets[pend+1] */
-      pend_o0 = o[0];
-      pend_o1 = o[1];
+    if (!pend_ok && b0 + rank < wg_hi) {
+      pend = b0 + rank;
+      /* only the low dwords: a batch is below 4 GiB, so offsets relative to
+       * `base` and lengths are exact modulo 2^32 */
+      const uint32_t *o = reinterpret_cast<const uint32_t *>(p.offsets + pend);
+      pend_o0 = *GLOBAL(const uint32_t, o);
+      pend_o1 = *GLOBAL(const uint32_t, o + 2);
       pend_ok = true;
     }
   };
@@ -274,28 +285,29 @@ __global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_ke
    * straight-line; the request-line record (once per request) and the header
    * record (every second event) are branches taken only by the lanes concerned */
   auto event = [&](bool valid, uint32_t ep, rhp_hdr_t *hout) {
-    const uint32_t k = d.k;
+    const uint32_t k = kn & 7u;
     if (valid) {
-      d.h23 = (d.h23 << 16) | (d.h01 >> 16);
-      d.h01 = (d.h01 << 16) | ep;
-      d.k = k == 4 ? 3u : k + 1u;
+      hx = (hx & 0xffff0000u) | (h01 >> 16);
+      h01 = (h01 << 16) | ep;
+      kn += k == 4 ? 0xffffffffu : 1u;
       /* CO: history = CO, prevLF; the max_headers check of the line start */
-      if (k == 3 && d.nh == maxh && d.ovf == 0) d.ovf = (d.h01 >> 16) + 2u;
+      if (k == 3 && (kn >> 8) == maxh && (hx >> 16) == 0) hx |= ((h01 >> 16) + 2u) << 16;
     }
     if (valid && k == 2) {   /* RL: history = RL, PE, ME */
-      const uint32_t pe = d.h01 >> 16, me = d.h23 & 0xffffu;
-      d.rl01 = me | ((me + 1u) << 16);
-      d.rl23 = (pe - me - 1u) | ((ep - pe - 9u) << 16);
-      d.h01 = (d.h01 & 0xffff0000u) | (pe + 10u);
+      const uint32_t pe = h01 >> 16, me = hx & 0xffffu;
+      rl = me | ((pe - me - 1u) << 16);
+      kn |= (ep - pe - 9u) << 3;
+      h01 = (h01 & 0xffff0000u) | (pe + 10u);
     }
     if (valid && k == 4) {   /* EOL: history = LF, CO, prevLF */
-      const uint32_t co = d.h01 >> 16, prev = d.h23 & 0xffffu;
+      const uint32_t co = h01 >> 16, prev = hx & 0xffffu;
       const uint32_t lo = (prev + 1u) | ((co - prev - 1u) << 16);
       const uint32_t hi = (co + 2u) | ((ep - co - 3u) << 16);
-      const uint32_t nh = ++d.nh;
+      kn += 256u;
+      const uint32_t nh = kn >> 8;
       if (nh <= maxh) {
         if (nh & 1u) { rec_lo = lo; rec_hi = hi; }
-        else if (!(p.pad & 2)) store_pair(hout + nh - 2u, u32x4{rec_lo, rec_hi, lo, hi});
+        else store_pair(hout + nh - 2u, u32x4{rec_lo, rec_hi, lo, hi});
       }
     }
   };
@@ -309,52 +321,55 @@ __global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_ke
    */
   auto decode = [&]() {
     if (!has) return;
-    const uint32_t row = st;
-    const bool slow = row == row_of(S_SLOW);
-    const bool term_ev = is_done_row(row) || is_err_row(row);
-    uint32_t m[kEvWords];
+    const uint32_t e = st;
+    const bool slow = is_slow8(e);
+    const bool term_ev = is_done8(e) || is_err8(e);
+    const int32_t block_pos = pos - (int32_t) kBlock;
+    uint64_t mh[kEvWords / 2];
 #pragma unroll
-    for (int w = 0; w < (int) kEvWords; w++) m[w] = slow ? 0u : ev[w];
+    for (int h = 0; h < (int) kEvWords / 2; h++) mh[h] = slow ? 0ull : (((uint64_t) ev[2 * h + 1] << 32) | ev[2 * h]);
     uint32_t term_pos = 0xffffffffu;
     if (term_ev) {   /* the terminal is the block's last event: take it off the mask */
       bool found = false;
 #pragma unroll
-      for (int w = (int) kEvWords - 1; w >= 0; w--) {
-        if (!found && m[w]) {
-          const uint32_t bt = 31u - __builtin_clz(m[w]);
-          term_pos = (uint32_t) block_pos + 32u * w + bt;
-          m[w] &= ~(1u << bt);
+      for (int h = (int) kEvWords / 2 - 1; h >= 0; h--) {
+        if (!found && mh[h]) {
+          const uint32_t bt = 63u - (uint32_t) __builtin_clzll(mh[h]);
+          term_pos = (uint32_t) (block_pos + 64 * h + (int32_t) bt);
+          mh[h] &= ~(1ull << bt);
           found = true;
         }
       }
     }
     rhp_hdr_t *hout = p.hdrs + (uint64_t) cur * maxh;
 #pragma unroll
-    for (int w = 0; w < (int) kEvWords; w++) {
-      uint32_t mw = d.ovf ? 0u : m[w];
-      while (__ballot(mw != 0)) {
-        const bool valid = mw != 0;
-        const uint32_t bt = __builtin_ctz(mw | 0x80000000u);
-        mw &= mw - 1u;
-        event(valid, (uint32_t) block_pos + 32u * w + bt, hout);
-        mw = d.ovf ? 0u : mw;
+    for (int h = 0; h < (int) kEvWords / 2; h++) {
+      uint64_t m = (hx >> 16) ? 0ull : mh[h];
+      while (__ballot(m != 0)) {
+        const bool valid = m != 0;
+        const uint32_t bt = (uint32_t) __builtin_ctzll(m | (1ull << 63));
+        m &= m - 1u;
+        event(valid, (uint32_t) (block_pos + 64 * h + (int32_t) bt), hout);
+        m = (hx >> 16) ? 0ull : m;
       }
     }
-    const bool ovf = d.ovf != 0;
-    const bool fin = ovf || slow || term_ev || pos >= (int32_t) cur_len;
+    const uint32_t ovf_at = hx >> 16;
+    const bool ovf = ovf_at != 0;
+    const bool fin = ovf || slow || term_ev || (uint32_t) pos >= cur_len;
     if (!fin) return;
-    const bool ok = !ovf && is_done_row(row) && term_pos < cur_len;
-    const bool bad = ovf ? d.ovf - 1u < cur_len : (is_err_row(row) && term_pos < cur_len);
+    const bool ok = !ovf && is_done8(e) && term_pos < cur_len;
+    const bool bad = ovf ? ovf_at - 1u < cur_len : (is_err8(e) && term_pos < cur_len);
     rhp_req_t r = {};
     r.minor_version = -1;
     if (ok) {
-      if ((d.nh & 1u) && !(p.pad & 2)) store_one(hout + d.nh - 1u, u32x2{rec_lo, rec_hi});
+      const uint32_t nh = kn >> 8;
+      if (nh & 1u) store_one(hout + nh - 1u, u32x2{rec_lo, rec_hi});
       r.ret = (int32_t) term_pos + 1;
-      r.method_len = (uint16_t) d.rl01;
-      r.path_off = (uint16_t) (d.rl01 >> 16);
-      r.path_len = (uint16_t) d.rl23;
-      r.minor_version = (int8_t) (d.rl23 >> 16);
-      r.num_headers = (uint16_t) d.nh;
+      r.method_len = (uint16_t) rl;
+      r.path_off = (uint16_t) (rl + 1u);
+      r.path_len = (uint16_t) (rl >> 16);
+      r.minor_version = (int8_t) ((kn >> 3) & 1u);
+      r.num_headers = (uint16_t) nh;
       r.flags = p.mode == RHP_MODE_HTTP ? (uint16_t) kDeferFrame : (uint16_t) 0;   /* framing: replay */
       if (p.mode == RHP_MODE_HTTP) *wg_deferred = 1u;
     } else if (bad) {
@@ -364,58 +379,45 @@ __global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_ke
       r.flags = (uint16_t) kDeferExact;   /* exact path: replay */
       *wg_deferred = 1u;
     }
-    if (!(p.pad & 2)) store_req(p.reqs + cur, r);
+    store_req(p.reqs + cur, r);
     has = false;
-    st = park;
+    st = kPark;
   };
 
-  /* 16 DFA steps over one 16-byte chunk; events -> bits [base, base+16) of ev */
-  auto steps = [&](const u32x4 &chunk, uint32_t &ev, const int base) {
+  /* 16 DFA steps over one 16-byte chunk; events shifted into ev.  The table
+   * sits at LDS address 0, so the v_perm result is the address itself. */
+  auto steps16 = [&](const u32x4 &chunk, uint32_t &ev) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const uint32_t c = (chunk[k >> 2] >> ((k & 3) * 8)) & 0xffu;
-      st = *reinterpret_cast<const uint16_t *>(lds + st + c * 2u);
-      ev_or(ev, st, base + k);
-      /* keep the scheduler from hoisting the byte extraction of all 64 steps
-       * (it would hold 64 VGPRs of precomputed offsets) */
-      if ((k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    for (int q = 0; q < 4; q++) {
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const uint32_t a = __builtin_amdgcn_perm(st, chunk[q], 0x0c0c0400u | (uint32_t) b);
+        st = *reinterpret_cast<const __attribute__((address_space(3))) uint8_t *>((size_t) a);
+        ev_shift(ev, st);
+      }
+      /* keep the scheduler from batching the event shifts of many steps
+       * (each would hold its step's state in a VGPR of its own) */
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
-  /* half h of the lane's window from the staging buffer (zeros for an idle lane) */
-  auto read_half = [&](uint32_t kind, int h) {
-    const uint8_t *sb = lds + stage + (kDoubleStage ? (buf ^ kStageBuf) : 0u);
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-      W[q] = kind ? *reinterpret_cast<const u32x4 *>(sb + stage_off(lane, 4 * h + q)) : u32x4{0, 0, 0, 0};
-  };
-
-  /* LDS-DMA of half h of every lane's next window (nw_ptr / nw_kind) */
-  auto issue_half = [&](int h) {
-    uint8_t *db = lds + stage + (kDoubleStage ? buf : 4096u * h);
-#ifdef RHP_OWN_WINDOW
-    /* experiment: every lane fetches its own window (lane-linear) */
-    if (nw_kind) {
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(p.bytes + nw_ptr + 64u * h + 16u * i),
-                                         (__attribute__((address_space(3))) void *) (db + 1024u * i), 16, 0, 0);
-    }
-#else
-    /* the wave fetches all 64 windows with 4 LDS-DMA loads, 16 windows of 64 B each */
-    const uint64_t src = nw_kind ? nw_ptr + 64u * h : ~(uint64_t) 0;
-    const uint32_t slo = (uint32_t) src, shi = (uint32_t) (src >> 32);
-    const uint32_t part = ((lane & 3u) - (lane >> 4)) & 3u;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const uint32_t w = 16u * i + (lane >> 2);
-      const uint32_t lo = __shfl(slo, (int) w), hi = __shfl(shi, (int) w);
-      const uint64_t a = ((uint64_t) hi << 32) | lo;
-      if (a != ~(uint64_t) 0)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(p.bytes + a + 16u * part),
-                                         (__attribute__((address_space(3))) void *) (db + 1024u * i), 16, 0, 0);
-    }
+  /* LDS-DMA of every lane's next window (nw) into the staging buffer:
+   * kParts loads of 1 KiB (see stage_off) */
+  auto issue_one = [&](int i) {
+    const uint32_t src = (nw & 3u) ? (nw & ~3u) : 0xffffffffu;
+    const uint32_t w = dma_window((uint32_t) i, lane);
+    const uint32_t part = dma_part(w, lane);
+    uint32_t a = (uint32_t) __shfl((int) src, (int) w);
+#ifdef RHP_EXP_HOTWIN   /* timing experiment (config 2 only): every request reads its range's first request */
+    if (a != 0xffffffffu) a &= 255u;
 #endif
+    if (a != 0xffffffffu)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(wbytes + a + 16u * part),
+                                       (__attribute__((address_space(3))) void *) (lds + stage + 1024u * i), 16, 0, 0);
+  };
+  auto issue = [&]() {
+#pragma unroll
+    for (int i = 0; i < (int) kParts; i++) issue_one(i);
   };
 
   refill_pend();
@@ -430,17 +432,17 @@ __global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_ke
    * loop's only VMEM wait -> [B] decode + finalize the previous block (its
    * stores are older than any load the next [A] waits for) -> [C] switch to the
    * landed window -> [D] hand out pending requests -> [E] issue the next
-   * window's loads -> 64 DFA steps.
+   * window's loads into the buffer [A] just read -> 64 DFA steps.
    */
   for (;;) {
     RHP_STAMP(t0);
     /* [A] */
-    const uint64_t p_o0 = pend_o0, p_o1 = pend_o1;
-    const uint32_t nw_kind_prev = nw_kind;
+    const uint32_t p_o0 = pend_o0, p_o1 = pend_o1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the window's LDS-DMA has landed */
-    read_half(nw_kind_prev, 0);
+#pragma unroll
+    for (int q = 0; q < kWRegs; q++) W[q] = *reinterpret_cast<const u32x4 *>(lds + stage + stage_off(lane, q));
 #ifdef RHP_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     RHP_STAMP(t1); acc[0] += t1 - t0; t0 = t1;
 #endif
     /* [B] */
@@ -449,18 +451,20 @@ __global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_ke
     RHP_STAMP(t1); acc[1] += t1 - t0; t0 = t1;
 #endif
     /* [C] */
+    const uint32_t nw_kind = nw & 3u;
     if (nw_kind == 2) {
-      cur = pend; cur_off = p_o0; cur_len = (uint32_t) min(p_o1 - p_o0, (uint64_t) 0xffffffffu);
+      cur = pend;
+      cur_len = p_o1 - p_o0;
       pend_ok = false;
       has = true;
-      const uint32_t mis = (uint32_t) cur_off & 3u;
+      const uint32_t mis = (uint32_t) p_o0 & 3u;
       uint32_t s0 = mis == 0 ? S_METHOD0 : mis == 1 ? S_SKIP1 : mis == 2 ? S_SKIP2 : S_SKIP3;
       if (cur_len > kFastMaxLen) s0 = S_SLOW;
-      st = row_of(s0);
+      st = idx8(s0);
       pos = -(int32_t) mis;
-      dec_reset(d);
+      h01 = hx = kn = rl = 0;
     }
-    if (nw_kind) cur_ptr = nw_ptr;
+    if (nw_kind) cur_ptr = nw & ~3u;
     const bool pend_ready = pend_ok;   /* assigned before this block: p_o0/p_o1 valid */
     /* [D] */
     refill_pend();
@@ -468,39 +472,45 @@ __global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_ke
     RHP_STAMP(t1); acc[2] += t1 - t0; t0 = t1;
 #endif
     /* [E] next window: continuation of cur, else the first window of a ready pend */
-    nw_kind = 0;
-    if (has && cur_ptr + kBlock < cur_off + cur_len) {
-      nw_ptr = cur_ptr + kBlock;
-      nw_kind = 1;
-    } else if (pend_ready) {
-      nw_ptr = p_o0 & ~(uint64_t) 3;
-      nw_kind = 2;
-    }
-    if (!kDoubleStage) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   /* [A]'s reads of this buffer are done */
-    issue_half(0);
-    if (kDoubleStage) buf ^= kStageBuf;
-    if (!__ballot(has || nw_kind || pend_ok)) break;
+    nw = 0;
+    if (has && (uint32_t) (pos + (int32_t) kBlock) < cur_len) nw = (cur_ptr + kBlock) | 1u;
+    else if (pend_ready) nw = ((p_o0 & ~3u) - (uint32_t) base) | 2u;
+    if (kBlock == 128) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   /* [A]'s reads of the buffer are done */
+#ifndef RHP_SPREAD_ISSUE
+    if (kBlock == 128) issue();
+#endif
+    if (!__ballot(has || nw || pend_ok)) break;
 #ifdef RHP_STAMPS
     RHP_STAMP(t1); acc[3] += t1 - t0; t0 = t1;
 #endif
-    /* kBlock steps (idle lanes step in the parked terminal state) */
-    block_pos = pos;
+    /* [F] 64 steps (idle lanes step in the parked terminal state); the second
+     * half of the window is read after the first 32, and only then is the
+     * buffer refilled with the next window */
 #pragma unroll
     for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
-    steps(W[0], ev[0], 0);
-    steps(W[1], ev[0], 16);
-    steps(W[2], ev[1], 0);
-    steps(W[3], ev[1], 16);
-    if (kHalves == 2) {
-      /* second half of this window, then refill that half with the next window's */
-      __builtin_amdgcn_sched_barrier(0);
-      read_half(nw_kind_prev, 1);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      issue_half(1);
-      steps(W[0], ev[kEvWords - 2], 0);
-      steps(W[1], ev[kEvWords - 2], 16);
-      steps(W[2], ev[kEvWords - 1], 0);
-      steps(W[3], ev[kEvWords - 1], 16);
+    if (kBlock == 64) {
+#ifndef RHP_EXP_NOSTEP   /* timing experiment: no DFA steps (requests never finish) */
+      steps16(W[0], ev[0]);
+      steps16(W[1], ev[0]);
+#endif
+#pragma unroll
+      for (int q = 0; q < 2; q++) W[q] = *reinterpret_cast<const u32x4 *>(lds + stage + stage_off(lane, q + 2));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   /* the buffer is read: refill it */
+      issue();
+#ifndef RHP_EXP_NOSTEP
+      steps16(W[0], ev[1]);
+      steps16(W[1], ev[1]);
+#endif
+    } else {
+#pragma unroll
+      for (int q = 0; q < kWRegs; q++) {
+#ifndef RHP_EXP_NOSTEP
+        steps16(W[q], ev[q >> 1]);
+#endif
+#ifdef RHP_SPREAD_ISSUE   /* one LDS-DMA of the next window per 16 steps */
+        issue_one(q);
+#endif
+      }
     }
     pos += (int32_t) kBlock;
 #ifdef RHP_STAMPS
@@ -524,8 +534,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_MIN_WAVES_PER_SIMD) void rhp_dfa_ke
    * workgroup walks its range, one request per thread, and finishes what
    * finalize deferred: the exact scalar path, and http_read_request framing of
    * DFA-parsed requests in http mode.  Nothing to do -> no pass at all. */
-#ifndef RHP_NO_REPLAY   /* timing experiment only: deferred requests stay unfinished */
   __syncthreads();
+#ifndef RHP_NO_REPLAY   /* register-pressure experiments only: deferred requests stay unfinished */
   if (*wg_deferred) {
     for (uint32_t i = wg_lo + tid; i < wg_hi; i += WAVES * 64) {
       const uint32_t f = p.reqs[i].flags;
@@ -590,7 +600,7 @@ int dfa_waves()
 {
   if (g_waves < 0) {
     const char *e = getenv("RHP_WAVES");
-    g_waves = e ? atoi(e) : 16;
+    g_waves = e ? atoi(e) : 8;
   }
   return g_waves;
 }
@@ -598,7 +608,7 @@ int dfa_waves()
 
 extern "C" {
 
-const char *rhp_version(void) { return "rhp 0.3.0 (gfx950)"; }
+const char *rhp_version(void) { return "rhp 0.4.0 (gfx950)"; }
 
 #ifdef RHP_STAMPS
 /* diagnostic build only: copy the per-wave section cycle sums (8192 x 8 u64) */
@@ -646,12 +656,10 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.max_headers = b->max_headers;
   prm.mode = b->mode;
   prm.span = 0;
-  {
-    const char *e = getenv("RHP_EXPERIMENT");   /* timing experiments only: breaks results */
-    prm.pad = e ? (uint32_t) atoi(e) : 0u;
-  }
 
-  if (g_impl == RHP_IMPL_EXACT) {
+  /* the DFA kernel addresses windows with u32 offsets from its range start;
+   * batches of 4 GiB or more take the exact kernel */
+  if (g_impl == RHP_IMPL_EXACT || b->bytes_size >= 0xFFFF0000ull) {
     uint32_t grid = (b->n + 255) / 256;
     if (grid > (uint32_t) g_cus * 8) grid = (uint32_t) g_cus * 8;
     hipLaunchKernelGGL(rhp_exact_kernel, dim3(grid), dim3(256), 0, s, prm);
@@ -660,8 +668,6 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   switch (dfa_waves()) {
   case 4: return launch_dfa<4>(prm, s);
   case 8: return launch_dfa<8>(prm, s);
-  case 11: return launch_dfa<11>(prm, s);
-  case 10: return launch_dfa<10>(prm, s);
   case 12: return launch_dfa<12>(prm, s);
   default: return launch_dfa<16>(prm, s);
   }

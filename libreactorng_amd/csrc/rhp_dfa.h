@@ -194,6 +194,110 @@ constexpr Table8 make_table8()
 }
 
 /*
+ * Pair form (what the kernel runs): two bytes per table read.  Every state's
+ * transition depends on a byte only through its class (15 classes, checked by
+ * classes_exact below), so a step over bytes (b0, b1) is one read at
+ *   idx * 256 + class(b0) * 16 + class(b1)
+ * of a u8 table whose entries are pair indices.  A pair index carries the
+ * state after both bytes and, in its low two bits, whether the transition on
+ * b0 / on b1 was an event; the kernel shifts those two bits into its event
+ * mask (v_alignbit by 2), so the mask is the same per-byte event mask as the
+ * one-byte form produces.
+ *   plain state s:  idx = 4s + e   (e = 0, or 1: event on b0 only)
+ *   event state s:  idx = 4(s - S_NUM_PLAIN) + e   (e = 2 or 3: event on b1)
+ * The byte-class table lives in an unused row (kClassRow).
+ */
+enum : uint32_t {
+  C_CTLX = 0, C_HT, C_LF, C_CR, C_SP, C_COLON, C_H, C_T, C_P, C_SLASH, C_DOT, C_0, C_1, C_TCHAR, C_OTHER,
+  kClasses
+};
+
+constexpr uint32_t byte_class(uint32_t c)
+{
+  if (c == '\t') return C_HT;
+  if (c == '\n') return C_LF;
+  if (c == '\r') return C_CR;
+  if (c_ctl(c)) return C_CTLX;
+  switch (c) {
+  case ' ': return C_SP;
+  case ':': return C_COLON;
+  case 'H': return C_H;
+  case 'T': return C_T;
+  case 'P': return C_P;
+  case '/': return C_SLASH;
+  case '.': return C_DOT;
+  case '0': return C_0;
+  case '1': return C_1;
+  default: return c_tchar(c) ? C_TCHAR : C_OTHER;
+  }
+}
+
+constexpr uint32_t class_rep(uint32_t k)   /* a byte of class k */
+{
+  constexpr uint8_t rep[kClasses] = {0x00, '\t', '\n', '\r', ' ', ':', 'H', 'T', 'P', '/', '.', '0', '1', '!', '"'};
+  return rep[k];
+}
+
+/* every byte behaves like its class representative in every state */
+constexpr bool classes_exact()
+{
+  for (uint32_t k = 0; k < kClasses; k++)
+    if (byte_class(class_rep(k)) != k) return false;
+  for (uint32_t s = 0; s < S_COUNT; s++)
+    for (uint32_t c = 0; c < 256; c++)
+      if (step(s, c) != step(s, class_rep(byte_class(c)))) return false;
+  return true;
+}
+static_assert(classes_exact(), "byte classes must not split any transition");
+
+RHP_DHD constexpr uint32_t idx2(uint32_t s, uint32_t e)
+{
+  return s < S_NUM_PLAIN ? 4u * s + e : 4u * (s - S_NUM_PLAIN) + e;
+}
+RHP_DHD constexpr uint32_t state2(uint32_t idx)
+{
+  return (idx & 2u) ? (idx >> 2) + S_NUM_PLAIN : idx >> 2;
+}
+enum : uint32_t {
+  kRows2 = 4u * (S_NUM_PLAIN - 1u) + 2u,          /* highest index (last plain state, e = 1) + 1 */
+  kClassRow = 4u * (S_COUNT - S_NUM_PLAIN) + 2u,   /* first index no state uses */
+  kTable2Bytes = kRows2 * 256u
+};
+static_assert(kClassRow < kRows2 && state2(kClassRow) >= S_COUNT, "class row is a hole");
+static_assert(kRows2 <= 256u, "indices are bytes");
+
+RHP_DHD constexpr bool is_done2(uint32_t i) { return state2(i) == S_DONE || state2(i) == S_DONE_E; }
+RHP_DHD constexpr bool is_err2(uint32_t i) { return state2(i) == S_ERR || state2(i) == S_ERR_E; }
+RHP_DHD constexpr bool is_slow2(uint32_t i) { return state2(i) == S_SLOW; }
+
+struct Table2 {
+  uint8_t b[kTable2Bytes];
+};
+
+constexpr Table2 make_table2()
+{
+  Table2 t{};
+  for (uint32_t i = 0; i < kTable2Bytes; i++) t.b[i] = (uint8_t) idx2(S_SLOW, 0);   /* unused rows */
+  for (uint32_t s = 0; s < S_COUNT; s++) {
+    const bool ev = s >= S_NUM_PLAIN;
+    for (uint32_t e = ev ? 2u : 0u; e < (ev ? 4u : 2u); e++) {
+      const uint32_t row = idx2(s, e) * 256u;
+      for (uint32_t k0 = 0; k0 < 16; k0++)
+        for (uint32_t k1 = 0; k1 < 16; k1++) {
+          uint32_t next = idx2(S_SLOW, 0);
+          if (k0 < kClasses && k1 < kClasses) {
+            const uint32_t s1 = step(s, class_rep(k0)), s2 = step(s1, class_rep(k1));
+            next = idx2(s2, (s1 >= S_NUM_PLAIN ? 1u : 0u) | (s2 >= S_NUM_PLAIN ? 2u : 0u));
+          }
+          t.b[row + k0 * 16u + k1] = (uint8_t) next;
+        }
+    }
+  }
+  for (uint32_t c = 0; c < 256; c++) t.b[kClassRow * 256u + c] = (uint8_t) byte_class(c);
+  return t;
+}
+
+/*
  * Event decoder state of one request.  hist holds the last four event positions
  * as u16: h01 = e0 | e1 << 16, h23 = e2 | e3 << 16 (e0 newest).
  */

@@ -1,7 +1,7 @@
 /*
  * rhp_emu.cpp -- CPU emulation of rhp_dfa_kernel, for tests only.
  *
- * Runs the same u8 transition table (rhp_dfa.h), the same 4-byte window alignment
+ * Runs the same pair transition table (rhp_dfa.h Table2), the same 4-byte window alignment
  * (SKIP states), the same 64-byte blocks with one event-mask decode per block
  * (rhp_dfa.h dec_event) and the same finalize decisions as the kernel, one
  * request at a time on the host.  Lets the DFA design be checked against
@@ -20,9 +20,9 @@ using namespace rhp;
 
 namespace {
 
-const Table8 &table()
+const Table2 &table()
 {
-  static const Table8 t = make_table8();
+  static const Table2 t = make_table2();
   return t;
 }
 
@@ -53,7 +53,8 @@ void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
 
 extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] or NULL */)
 {
-  const Table8 &T = table();
+  const Table2 &T = table();
+  const uint8_t *cls = T.b + kClassRow * 256u;
   Stats st_count = {0, 0, 0};
   const uint32_t maxh = b->max_headers;
 
@@ -64,7 +65,7 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
     int32_t pos = -(int32_t) mis;
     uint32_t s0 = mis == 0 ? S_METHOD0 : mis == 1 ? S_SKIP1 : mis == 2 ? S_SKIP2 : S_SKIP3;
     if (len > kFastMaxLen) s0 = S_SLOW;
-    uint32_t st = idx8(s0);
+    uint32_t st = idx2(s0, 0);
     Dec d;
     dec_reset(d);
     rhp_hdr_t *hout = b->hdrs + (uint64_t) i * maxh;
@@ -74,16 +75,16 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
       uint64_t evw[RHP_BLOCK / 64];
       for (int w = 0; w < RHP_BLOCK / 64; w++) {
         uint64_t ev = 0;
-        for (int k = 0; k < 64; k++) {
-          st = T.b[st * 256u + win[64 * w + k]];
-          ev |= (uint64_t) (st & 1u) << k;
+        for (int k = 0; k < 64; k += 2) {   /* one table read per byte pair */
+          st = T.b[st * 256u + cls[win[64 * w + k]] * 16u + cls[win[64 * w + k + 1]]];
+          ev |= (uint64_t) (st & 3u) << k;
         }
         evw[w] = ev;
       }
       win += RHP_BLOCK;
       pos += RHP_BLOCK;
-      const bool slow = is_slow8(st);
-      const bool term_ev = is_done8(st) || is_err8(st);
+      const bool slow = is_slow2(st);
+      const bool term_ev = is_done2(st) || is_err2(st);
       uint32_t term_pos = 0xffffffffu;
       if (term_ev) {   /* the terminal is the block's last event */
         for (int w = RHP_BLOCK / 64 - 1; w >= 0; w--)
@@ -112,8 +113,8 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
       const bool ovf = d.ovf != 0;
       if (!(ovf || slow || term_ev || pos >= (int32_t) len)) continue;
       /* ---- finalize (same decisions as the kernel) ---- */
-      const bool ok = !ovf && is_done8(st) && term_pos < len;
-      const bool bad = ovf ? d.ovf - 1u < len : (is_err8(st) && term_pos < len);
+      const bool ok = !ovf && is_done2(st) && term_pos < len;
+      const bool bad = ovf ? d.ovf - 1u < len : (is_err2(st) && term_pos < len);
       if (ok) {
         st_count.fast_ok++;
         rhp_req_t r;

@@ -40,7 +40,7 @@ namespace {
 
 using namespace rhp;
 
-__device__ const Table8 g_table8 = make_table8();
+__device__ const Table2 g_table2 = make_table2();
 
 struct Params {
   const uint8_t *bytes;
@@ -64,14 +64,14 @@ enum : uint32_t {
   kBlock = RHP_BLOCK,                            /* window bytes per lane per loop iteration (64 or 128) */
   kParts = kBlock / 16,                          /* 16-byte parts per window */
   kEvWords = kBlock / 32,                        /* 32-bit event words per block */
-  kLdsTable = (kTable8Bytes + 1023u) & ~1023u,  /* staging starts 1 KiB aligned */
+  kLdsTable = (kTable2Bytes + 1023u) & ~1023u,  /* staging starts 1 KiB aligned */
   kStageWave = 64 * kBlock,                      /* one window per lane, single-buffered */
-  kPark = 0,                                     /* idx8(S_DONE): idle lanes step here */
+  kPark = 0,                                     /* idx2(S_DONE, 0): idle lanes step here */
   kDeferExact = 0x8000u,                         /* reqs[i].flags while deferred (kernel-internal) */
   kDeferFrame = 0x4000u
 };
 static_assert(kBlock == 64 || kBlock == 128, "64- or 128-byte windows");
-static_assert(idx8(S_DONE) == kPark, "parked lanes sit in DONE");
+static_assert(idx2(S_DONE, 0) == kPark, "parked lanes sit in DONE");
 
 /* LDS byte address of part q (16 B) of lane w's window inside the staging
  * buffer.  The LDS-DMA loads of a wave write lane-linearly (1 KiB per
@@ -151,13 +151,19 @@ __device__ __forceinline__ void finish_http(const Params &p, uint32_t i, uint64_
  * global_store (VM counter only), not flat_store (VM + LGKM). */
 #define GLOBAL(T, x) ((__attribute__((address_space(1))) T *) (x))
 
-/* ev = (ev >> 1) | (st << 31): bit 0 of the state index (the event bit) into
- * the top of the mask.  Written as asm so the compiler cannot sink the shifts
- * of a block's steps into one chain at its end, which would keep every step's
- * state alive in its own VGPR. */
-__device__ __forceinline__ void ev_shift(uint32_t &ev, uint32_t st)
+/* ev = (ev >> 2) | (idx << 30): the two event bits of a pair index (b0 ->
+ * bit 30, b1 -> bit 31) into the top of the mask.  Written as asm so the
+ * compiler cannot sink the shifts of a block's steps into one chain at its
+ * end, which would keep every step's index alive in its own VGPR. */
+__device__ __forceinline__ void ev_shift2(uint32_t &ev, uint32_t idx)
 {
-  asm("v_alignbit_b32 %0, %1, %0, 1" : "+v"(ev) : "v"(st));
+  asm("v_alignbit_b32 %0, %1, %0, 2" : "+v"(ev) : "v"(idx));
+}
+
+/* one byte of LDS at address a (the table is at LDS address 0) */
+__device__ __forceinline__ uint32_t lds_u8(uint32_t a)
+{
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint8_t *>((size_t) a);
 }
 
 /* a 16-byte header-record pair, or a single record, at 4-byte alignment */
@@ -206,9 +212,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #endif
 
   {
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(&g_table8);
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(&g_table2);
     u32x4 *dst = reinterpret_cast<u32x4 *>(lds);
-    for (uint32_t k = tid; k < kTable8Bytes / 16; k += WAVES * 64) dst[k] = src[k];
+    for (uint32_t k = tid; k < kTable2Bytes / 16; k += WAVES * 64) dst[k] = src[k];
     if (tid < 2) reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave)[tid] = 0;   /* pool counter, replay flag */
   }
   __syncthreads();
@@ -231,7 +237,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   const uint8_t *wbytes = p.bytes + base;
 
   /* ---- lane state ---- */
-  uint32_t st = kPark;                 /* u8 state index */
+  uint32_t st = kPark;                 /* pair index (rhp_dfa.h idx2) */
   int32_t pos = 0;                     /* request-relative position of the next byte to step */
   uint32_t ev[kEvWords];               /* events of the block just stepped (32 bytes per word) */
 #pragma unroll
@@ -322,8 +328,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   auto decode = [&]() {
     if (!has) return;
     const uint32_t e = st;
-    const bool slow = is_slow8(e);
-    const bool term_ev = is_done8(e) || is_err8(e);
+    const bool slow = is_slow2(e);
+    const bool term_ev = is_done2(e) || is_err2(e);
     const int32_t block_pos = pos - (int32_t) kBlock;
     uint64_t mh[kEvWords / 2];
 #pragma unroll
@@ -357,8 +363,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const bool ovf = ovf_at != 0;
     const bool fin = ovf || slow || term_ev || (uint32_t) pos >= cur_len;
     if (!fin) return;
-    const bool ok = !ovf && is_done8(e) && term_pos < cur_len;
-    const bool bad = ovf ? ovf_at - 1u < cur_len : (is_err8(e) && term_pos < cur_len);
+    const bool ok = !ovf && is_done2(e) && term_pos < cur_len;
+    const bool bad = ovf ? ovf_at - 1u < cur_len : (is_err2(e) && term_pos < cur_len);
     rhp_req_t r = {};
     r.minor_version = -1;
     if (ok) {
@@ -384,20 +390,46 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     st = kPark;
   };
 
-  /* 16 DFA steps over one 16-byte chunk; events shifted into ev.  The table
-   * sits at LDS address 0, so the v_perm result is the address itself. */
-  auto steps16 = [&](const u32x4 &chunk, uint32_t &ev) {
+  /* The table sits at LDS address 0, so a v_perm result is the address itself.
+   * classes16: the byte classes of a 16-byte chunk (16 independent reads of
+   * the class row); codes: pair codes class(b0)*16 + class(b1), two per dword;
+   * steps16: 8 chained pair steps, two event bits each shifted into ev. */
+  auto classes16 = [&](const u32x4 &chunk, uint32_t (&k)[16]) {
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int b = 0; b < 4; b++)
+        k[4 * q + b] = lds_u8(__builtin_amdgcn_perm(kClassRow, chunk[q], 0x0c0c0400u | (uint32_t) b));
+  };
+  auto codes = [&](const uint32_t (&k)[16], uint32_t (&pc)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      pc[q] = ((k[4 * q] << 4) | k[4 * q + 1]) | (((k[4 * q + 2] << 4) | k[4 * q + 3]) << 8);
+  };
+  auto steps16 = [&](const uint32_t (&pc)[4], uint32_t &ev) {
 #pragma unroll
     for (int q = 0; q < 4; q++) {
 #pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const uint32_t a = __builtin_amdgcn_perm(st, chunk[q], 0x0c0c0400u | (uint32_t) b);
-        st = *reinterpret_cast<const __attribute__((address_space(3))) uint8_t *>((size_t) a);
-        ev_shift(ev, st);
+      for (int j = 0; j < 2; j++) {
+        st = lds_u8(__builtin_amdgcn_perm(st, pc[q], 0x0c0c0400u | (uint32_t) j));
+        ev_shift2(ev, st);
       }
-      /* keep the scheduler from batching the event shifts of many steps
-       * (each would hold its step's state in a VGPR of its own) */
+    }
+  };
+  /* a window's 16-byte chunks: the class reads of chunk q+1 are issued before
+   * the chained steps of chunk q, so their latency hides behind the chain */
+  auto steps_chunks = [&](const u32x4 *Wc, int nchunks, uint32_t *evw) {
+    uint32_t k[16], pc[4];
+    classes16(Wc[0], k);
+    codes(k, pc);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      if (q >= nchunks) break;
+      if (q + 1 < nchunks) classes16(Wc[q + 1], k);
       __builtin_amdgcn_sched_barrier(0);
+      steps16(pc, evw[q >> 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (q + 1 < nchunks) codes(k, pc);
     }
   };
 
@@ -460,7 +492,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const uint32_t mis = (uint32_t) p_o0 & 3u;
       uint32_t s0 = mis == 0 ? S_METHOD0 : mis == 1 ? S_SKIP1 : mis == 2 ? S_SKIP2 : S_SKIP3;
       if (cur_len > kFastMaxLen) s0 = S_SLOW;
-      st = idx8(s0);
+      st = idx2(s0, 0);
       pos = -(int32_t) mis;
       h01 = hx = kn = rl = 0;
     }
@@ -476,9 +508,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     if (has && (uint32_t) (pos + (int32_t) kBlock) < cur_len) nw = (cur_ptr + kBlock) | 1u;
     else if (pend_ready) nw = ((p_o0 & ~3u) - (uint32_t) base) | 2u;
     if (kBlock == 128) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   /* [A]'s reads of the buffer are done */
-#ifndef RHP_SPREAD_ISSUE
     if (kBlock == 128) issue();
-#endif
     if (!__ballot(has || nw || pend_ok)) break;
 #ifdef RHP_STAMPS
     RHP_STAMP(t1); acc[3] += t1 - t0; t0 = t1;
@@ -490,27 +520,19 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
     if (kBlock == 64) {
 #ifndef RHP_EXP_NOSTEP   /* timing experiment: no DFA steps (requests never finish) */
-      steps16(W[0], ev[0]);
-      steps16(W[1], ev[0]);
+      steps_chunks(W, 2, ev);
 #endif
 #pragma unroll
       for (int q = 0; q < 2; q++) W[q] = *reinterpret_cast<const u32x4 *>(lds + stage + stage_off(lane, q + 2));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   /* the buffer is read: refill it */
       issue();
 #ifndef RHP_EXP_NOSTEP
-      steps16(W[0], ev[1]);
-      steps16(W[1], ev[1]);
+      steps_chunks(W, 2, ev + 1);
 #endif
     } else {
-#pragma unroll
-      for (int q = 0; q < kWRegs; q++) {
 #ifndef RHP_EXP_NOSTEP
-        steps16(W[q], ev[q >> 1]);
+      steps_chunks(W, 8, ev);
 #endif
-#ifdef RHP_SPREAD_ISSUE   /* one LDS-DMA of the next window per 16 steps */
-        issue_one(q);
-#endif
-      }
     }
     pos += (int32_t) kBlock;
 #ifdef RHP_STAMPS
@@ -600,7 +622,7 @@ int dfa_waves()
 {
   if (g_waves < 0) {
     const char *e = getenv("RHP_WAVES");
-    g_waves = e ? atoi(e) : 8;
+    g_waves = e ? atoi(e) : 16;
   }
   return g_waves;
 }

@@ -1,0 +1,429 @@
+/*
+ * server.c -- the HTTP server of the libreactor surface (reference
+ * src/reactor/server.c, server.h:37-45) with the receive path on the MI355X
+ * batch parser.
+ *
+ * The reference parses a session synchronously when its recv completes
+ * (server_session_read, server.c:37-65): parse, SERVER_REQUEST, repeat while
+ * the session is READY, then flush.  Here a session that received bytes is
+ * queued, and once per reactor round (a reactor_next call) every queued
+ * session's unconsumed input is parsed in ONE batch (batch.c), after which
+ * SERVER_REQUEST is dispatched per request in session order -- the same flags
+ * (READY / PROCESSING), the same abort handling, the same -1 -> close and
+ * 0 -> wait outcomes.
+ *
+ * Pipelined input: a session's input is split
+ * speculatively after every "\r\n\r\n" and each piece is one request of the
+ * batch, so N pipelined requests cost one launch, not N.  A piece's result is
+ * taken when it is the last piece (its length is the rest of the input, as
+ * for http_read_request) or when it parsed as one complete request that ends
+ * exactly at the next piece; otherwise (a body, LF-only line ends, ...) the
+ * rest of that session's input is parsed again, whole, in the next batch.
+ */
+#include <stddef.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "reactor.h"
+#include "reactor_batch.h"
+#include "rhp.h"
+
+#define container_of(p, T, m) ((T *) ((char *) (p) - offsetof(T, m)))
+
+static void list_init(list_t *l) { l->next = l->prev = l; }
+static bool list_is_empty(const list_t *l) { return l->next == l; }
+static void list_push(list_t *head, list_t *node)
+{
+  node->prev = head->prev;
+  node->next = head;
+  head->prev->next = node;
+  head->prev = node;
+}
+static void list_unlink(list_t *node)
+{
+  node->prev->next = node->next;
+  node->next->prev = node->prev;
+  list_init(node);
+}
+
+/* ---------------------------------------------------------------- date */
+
+static __thread char server_date[30];
+
+static void server_date_update(void)
+{
+  static const char days[] = "SunMonTueWedThuFriSat", months[] = "JanFebMarAprMayJunJulAugSepOctNovDec";
+  time_t t = (time_t) ((reactor_now() + 10000000) / 1000000000);
+  struct tm tm;
+  char text[64];
+  (void) gmtime_r(&t, &tm);
+  snprintf(text, sizeof text, "%.3s, %02d %.3s %04d %02d:%02d:%02d GMT", days + 3 * tm.tm_wday, tm.tm_mday,
+           months + 3 * tm.tm_mon, tm.tm_year + 1900, tm.tm_hour, tm.tm_min, tm.tm_sec);
+  memcpy(server_date, text, 29);   /* "Wed, 16 Aug 2023 10:29:23 GMT" */
+}
+
+/* ------------------------------------------------------------- session */
+
+static void server_batch_run(reactor_event_t *);
+
+static void server_queue(server_session_t *s)
+{
+  server_t *server = s->server;
+  if (list_is_empty(&s->queued))
+    list_push(&server->queue, &s->queued);
+  if (!server->batch)
+    server->batch = reactor_next(server_batch_run, server);
+}
+
+/* a session taking part in a batch round is only marked; the round frees it */
+static void server_session_free(server_session_t *s)
+{
+  stream_destruct(&s->stream);
+  list_unlink(&s->link);
+  list_unlink(&s->queued);
+  if (s->in_round)
+    s->dead = true;
+  else
+    free(s);
+}
+
+static void server_session_close(server_session_t *s)
+{
+  stream_close(&s->stream);
+  if (s->abort)
+    *s->abort = true;
+  if (s->next)
+  {
+    reactor_cancel(s->next, NULL, NULL);
+    s->next = 0;
+  }
+  list_unlink(&s->queued);
+  if (s->flags & SERVER_SESSION_READY)
+    server_session_free(s);
+}
+
+static void server_session_next(reactor_event_t *event)
+{
+  server_session_t *s = event->state;
+  s->next = 0;
+  server_queue(s);
+}
+
+static void server_session_stream(reactor_event_t *event)
+{
+  server_session_t *s = event->state;
+  if (reactor_likely(event->type == STREAM_READ))
+    server_queue(s);
+  else
+    server_session_close(s);
+}
+
+static void server_create_session(server_t *server, int fd)
+{
+  server_session_t *s = calloc(1, sizeof *s);
+  if (!s)
+    abort();
+  s->user = server->user;
+  s->flags = SERVER_SESSION_READY;
+  s->server = server;
+  list_init(&s->queued);
+  list_push(&server->sessions, &s->link);
+  stream_construct(&s->stream, server_session_stream, s);
+  stream_open(&s->stream, fd, 0);
+}
+
+static void server_accept(reactor_event_t *event)
+{
+  server_t *server = event->state;
+  switch (event->type)
+  {
+  case NETWORK_ACCEPT:
+    server_create_session(server, (int) event->data);
+    break;
+  case NETWORK_ACCEPT_BIND:
+    break;
+  default:
+    server->accept = 0;
+    reactor_call(&server->user, SERVER_ERROR, 0);
+    break;
+  }
+}
+
+static void server_timeout(reactor_event_t *event)
+{
+  (void) event;
+  server_date_update();
+}
+
+/* --------------------------------------------------------------- batch */
+
+typedef struct piece
+{
+  server_session_t *session;
+  uint64_t          start;   /* offset in the session's unconsumed input */
+  uint64_t          len;
+  uint32_t          index;   /* request index in the batch */
+  bool              last;
+} piece_t;
+
+typedef struct round
+{
+  server_session_t **sessions;
+  size_t             n_sessions, cap_sessions;
+  piece_t           *pieces;
+  size_t             n_pieces, cap_pieces;
+} round_t;
+
+static void *grow(void *p, size_t *cap, size_t need, size_t elem)
+{
+  if (need <= *cap)
+    return p;
+  size_t c = *cap ? *cap * 2 : 64;
+  while (c < need)
+    c *= 2;
+  p = realloc(p, c * elem);
+  if (!p)
+    abort();
+  *cap = c;
+  return p;
+}
+
+static const uint8_t *find_crlfcrlf(const uint8_t *p, const uint8_t *end)
+{
+  while (end - p >= 4)
+  {
+    const uint8_t *q = memchr(p + 3, '\n', (size_t) (end - p - 3));
+    if (!q)
+      return NULL;
+    if (q[-1] == '\r' && q[-2] == '\n' && q[-3] == '\r')
+      return q + 1;
+    p = q - 2;
+  }
+  return NULL;
+}
+
+/* dispatch the parsed pieces of one session in order; false: needs another
+ * batch over the rest of its input */
+static bool server_session_dispatch(server_session_t *s, const piece_t *pc, size_t np,
+                                    const reactor_batch_result_t *res)
+{
+  bool abort = false;
+  uint64_t at = 0;
+  size_t k = 0;
+  bool more = false;
+  while (s->flags & SERVER_SESSION_READY)
+  {
+    data_t in = stream_read(&s->stream);
+    if (k == np)
+    {
+      more = !data_empty(in);   /* requests left behind a trusted piece: parse the rest */
+      break;
+    }
+    const piece_t *p = &pc[k];
+    const rhp_http_t *x = &res->http[p->index];
+    if (p->start != at || !(p->last || (x->result == 1 && x->consumed == p->len)))
+    {
+      more = true;
+      break;
+    }
+    if (x->result == -1)
+    {
+      server_session_close(s);
+      return true;
+    }
+    if (x->result == 0)
+      break;
+    const uint64_t off = reactor_batch_offsets()[p->index];
+    uint8_t *base = data_base(in);
+    if (x->body_kind && x->consumed != (uint64_t) res->reqs[p->index].ret + x->body_len)
+      memcpy(base, res->bytes + off, x->consumed);   /* chunked body, de-framed in place */
+    reactor_http_fill(base, &res->reqs[p->index], res->hdrs + (size_t) p->index * REACTOR_BATCH_HEADERS, x,
+                      &s->request.method, &s->request.target, &s->request.body, s->request.fields,
+                      &s->request.fields_count);
+    stream_consume(&s->stream, x->consumed);
+    at += x->consumed;
+    k++;
+    s->flags &= ~SERVER_SESSION_READY;
+    s->flags |= SERVER_SESSION_PROCESSING;
+    s->abort = &abort;
+    reactor_call(&s->user, SERVER_REQUEST, (uintptr_t) s);
+    if (reactor_unlikely(abort))
+      return true;
+    s->abort = NULL;
+    s->flags &= ~SERVER_SESSION_PROCESSING;
+  }
+  stream_flush(&s->stream);
+  return !more;
+}
+
+static void server_batch_round(server_t *server, round_t *r)
+{
+  r->n_sessions = r->n_pieces = 0;
+  size_t bytes = 0;
+  while (!list_is_empty(&server->queue))
+  {
+    server_session_t *s = container_of(server->queue.next, server_session_t, queued);
+    list_unlink(&s->queued);
+    if (!(s->flags & SERVER_SESSION_READY) || !stream_is_open(&s->stream))
+      continue;
+    r->sessions = grow(r->sessions, &r->cap_sessions, r->n_sessions + 1, sizeof *r->sessions);
+    r->sessions[r->n_sessions++] = s;
+    s->in_round = true;
+    data_t in = stream_read(&s->stream);
+    const uint8_t *b = data_base(in), *end = b + data_size(in), *p = b;
+    while (p < end)
+    {
+      const uint8_t *q = s->exact ? NULL : find_crlfcrlf(p, end);
+      if (!q || q == end)
+        q = end;
+      r->pieces = grow(r->pieces, &r->cap_pieces, r->n_pieces + 1, sizeof *r->pieces);
+      const uint32_t index = (uint32_t) r->n_pieces;
+      r->pieces[index] = (piece_t) {.session = s, .start = (uint64_t) (p - b), .len = (uint64_t) (q - p),
+                                    .index = index, .last = q == end};
+      r->n_pieces = index + 1u;
+      p = q;
+    }
+    s->exact = false;
+    bytes += data_size(in);
+  }
+  if (!r->n_sessions)
+    return;
+
+  /* pack every session's input, back to back, and parse all pieces at once */
+  if (r->n_pieces)
+  {
+    uint8_t *h = reactor_batch_reserve(bytes, (uint32_t) r->n_pieces);
+    uint64_t *off = reactor_batch_offsets();
+    size_t at = 0, k = 0;
+    for (size_t i = 0; i < r->n_sessions; i++)
+    {
+      data_t in = stream_read(&r->sessions[i]->stream);
+      memcpy(h + at, data_base(in), data_size(in));
+      for (; k < r->n_pieces && r->pieces[k].session == r->sessions[i]; k++)
+        off[k] = at + r->pieces[k].start;
+      at += data_size(in);
+    }
+  }
+  reactor_batch_result_t res = {0};
+  if (r->n_pieces)
+    (void) reactor_batch_run((uint32_t) r->n_pieces, bytes, &res);
+
+  size_t k = 0;
+  for (size_t i = 0; i < r->n_sessions; i++)
+  {
+    server_session_t *s = r->sessions[i];
+    size_t k0 = k;
+    while (k < r->n_pieces && r->pieces[k].session == s)
+      k++;
+    if (!s->dead && !server_session_dispatch(s, r->pieces + k0, k - k0, &res) && !s->dead)
+    {
+      s->exact = true;   /* parse the rest as one piece (exact http_read_request semantics) */
+      server_queue(s);
+    }
+  }
+  for (size_t i = 0; i < r->n_sessions; i++)
+  {
+    r->sessions[i]->in_round = false;
+    if (r->sessions[i]->dead)
+      free(r->sessions[i]);
+  }
+}
+
+static void server_batch_run(reactor_event_t *event)
+{
+  server_t *server = event->state;
+  round_t r = {0};
+  server->batch = 0;
+  server_batch_round(server, &r);
+  free(r.sessions);
+  free(r.pieces);
+}
+
+/* -------------------------------------------------------------- public */
+
+void server_construct(server_t *server, reactor_callback_t *callback, void *state)
+{
+  *server = (server_t) {.user = reactor_user_define(callback, state)};
+  list_init(&server->sessions);
+  list_init(&server->queue);
+  timeout_construct(&server->timeout, server_timeout, NULL);
+}
+
+void server_destruct(server_t *server)
+{
+  server_close(server);
+  timeout_destruct(&server->timeout);
+  while (!list_is_empty(&server->sessions))
+  {
+    server_session_t *s = container_of(server->sessions.next, server_session_t, link);
+    if (s->next)
+      reactor_cancel(s->next, NULL, NULL);
+    if (s->abort)
+      *s->abort = true;
+    server_session_free(s);
+  }
+  if (server->batch)
+    reactor_cancel(server->batch, NULL, NULL);
+  server->batch = 0;
+}
+
+void server_open(server_t *server, const char *host, int port)
+{
+  server->accept = network_accept(server_accept, server, host, port, NETWORK_REUSEADDR);
+  timeout_set(&server->timeout, (reactor_now() / 1000000000) * 1000000000, 1000000000);
+  server_date_update();
+}
+
+void server_open_socket(server_t *server, int socket)
+{
+  server->accept = network_accept_socket(server_accept, server, socket);
+  timeout_set(&server->timeout, (reactor_now() / 1000000000) * 1000000000, 1000000000);
+  server_date_update();
+}
+
+void server_close(server_t *server)
+{
+  if (server->accept)
+  {
+    network_cancel(server->accept);
+    server->accept = 0;
+  }
+  timeout_clear(&server->timeout);
+}
+
+void server_disconnect(server_session_t *session)
+{
+  session->flags |= SERVER_SESSION_READY;
+  server_session_close(session);
+}
+
+void server_respond(server_session_t *session, string_t status, string_t type, data_t body, http_field_t *fields,
+                    size_t fields_count)
+{
+  session->flags |= SERVER_SESSION_READY;
+  if (reactor_likely(stream_is_open(&session->stream)))
+  {
+    http_write_response(&session->stream, status, data(server_date, 29), type, body, fields, fields_count);
+    if (!(session->flags & SERVER_SESSION_PROCESSING))
+    {
+      stream_flush(&session->stream);
+      session->next = reactor_next(server_session_next, session);
+    }
+  }
+  else
+  {
+    server_session_close(session);
+  }
+}
+
+void server_ok(server_session_t *session, string_t type, string_t body, http_field_t *fields, size_t fields_count)
+{
+  server_respond(session, string("200 OK"), type, body, fields, fields_count);
+}
+
+void server_plain(server_session_t *session, data_t body, http_field_t *fields, size_t fields_count)
+{
+  server_respond(session, string("200 OK"), string("text/plain"), body, fields, fields_count);
+}

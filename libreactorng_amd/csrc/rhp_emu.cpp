@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "rhp.h"
+#include "rhp_host.h"
 #include "rhp_dfa.h"
 #include "rhp_scalar.h"
 

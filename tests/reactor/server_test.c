@@ -1,0 +1,311 @@
+/*
+ * server_test.c -- end-to-end test of libreactor.so's HTTP server over
+ * loopback: the server runs in the reactor loop of the main thread (its
+ * sessions parsed in batches by the parser RHP_REACTOR_PARSER selects); a
+ * client thread plays the cases of the reference's test/server.c:150-160 (same
+ * requests, same callback behaviour: /abort, /next1, /next2, invalid input,
+ * an immediate close) plus BASELINE config 1 (16 pipelined 128-byte GETs in one
+ * write), request bodies (Content-Length and chunked) and a many-connection
+ * pipelined load.
+ * usage: server_test [connections] [requests-per-connection]; exit 0 = pass.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+
+#include "reactor.h"
+
+static int port;
+static int stop_pipe[2];
+static atomic_long calls;
+static int failures;
+
+#define CHECK(cond, ...) do { if (!(cond)) { failures++; printf("FAIL %s:%d: ", __FILE__, __LINE__); printf(__VA_ARGS__); printf("\n"); fflush(stdout); } } while (0)
+
+/* ---------------------------------------------------------------- server */
+
+static void server_next1(reactor_event_t *event)
+{
+  server_respond((server_session_t *) event->state, string("200 OK"), string("text/plain"), string("ok"), NULL, 0);
+}
+
+static void server_next2(reactor_event_t *event)
+{
+  server_session_t *session = (server_session_t *) event->state;
+  server_ok(session, string("text/plain"), string("ok"), NULL, 0);
+  server_disconnect(session);
+}
+
+static void server_callback(reactor_event_t *event)
+{
+  server_session_t *session = (server_session_t *) event->data;
+  atomic_fetch_add(&calls, 1);
+  if (event->type != SERVER_REQUEST)
+    return;
+  if (string_equal(session->request.target, string("/abort")))
+  {
+    server_plain(session, string("no"), NULL, 0);
+    server_disconnect(session);
+  }
+  else if (string_equal(session->request.target, string("/next1")))
+    reactor_next(server_next1, session);
+  else if (string_equal(session->request.target, string("/next2")))
+    reactor_next(server_next2, session);
+  else if (string_equal(session->request.target, string("/body")))
+    server_plain(session, session->request.body, NULL, 0);   /* echo the request body */
+  else
+    server_plain(session, string("ok"), NULL, 0);
+}
+
+static server_t server;
+
+static void stop_ready(reactor_event_t *event)
+{
+  reactor_poll_remove(*(reactor_t *) event->state);
+  server_destruct(&server);
+}
+
+/* ---------------------------------------------------------------- client */
+
+static int client(void)
+{
+  struct sockaddr_in sin = {.sin_family = AF_INET, .sin_addr.s_addr = htonl(0x7f000001), .sin_port = htons(port)};
+  int c = socket(AF_INET, SOCK_STREAM, 0);
+  struct timeval tv = {.tv_sec = 10};
+  (void) setsockopt(c, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+  (void) setsockopt(c, IPPROTO_TCP, TCP_NODELAY, (int[]) {1}, sizeof(int));
+  if (connect(c, (struct sockaddr *) &sin, sizeof sin) != 0)
+  {
+    CHECK(0, "connect: %s", strerror(errno));
+    close(c);
+    return -1;
+  }
+  return c;
+}
+
+static void send_all(int c, const char *p, size_t n)
+{
+  while (n)
+  {
+    ssize_t k = send(c, p, n, MSG_NOSIGNAL);
+    if (k <= 0)
+      return;
+    p += k;
+    n -= (size_t) k;
+  }
+}
+
+typedef struct reader
+{
+  char    buf[1 << 16];
+  size_t  len;
+  int     eof;
+} reader_t;
+
+/* one response: status code, body into `body` (NUL-terminated); 0 on EOF/timeout */
+static int read_response(int c, reader_t *r, char *body, size_t cap)
+{
+  for (;;)
+  {
+    char *end = memmem(r->buf, r->len, "\r\n\r\n", 4);
+    if (end)
+    {
+      size_t head = (size_t) (end - r->buf) + 4;
+      char *cl = memmem(r->buf, head, "Content-Length: ", 16);
+      size_t blen = cl ? strtoul(cl + 16, NULL, 10) : 0;
+      if (r->len >= head + blen)
+      {
+        int code = strncmp(r->buf, "HTTP/1.1 ", 9) == 0 ? atoi(r->buf + 9) : -1;
+        size_t k = blen < cap - 1 ? blen : cap - 1;
+        memcpy(body, r->buf + head, k);
+        body[k] = 0;
+        memmove(r->buf, r->buf + head + blen, r->len - head - blen);
+        r->len -= head + blen;
+        return code;
+      }
+    }
+    if (r->eof)
+      return 0;
+    ssize_t n = recv(c, r->buf + r->len, sizeof r->buf - r->len, 0);
+    if (n <= 0)
+    {
+      r->eof = 1;
+      if (r->len == 0)
+        return 0;
+    }
+    else
+      r->len += (size_t) n;
+  }
+}
+
+static int at_eof(int c, reader_t *r)
+{
+  if (r->len)
+    return 0;
+  char x;
+  ssize_t n = recv(c, &x, 1, 0);
+  return n == 0;
+}
+
+/* one case: send `req`, expect `responses` 200s with body `want` (NULL: any), then EOF or not */
+static void run_case(const char *name, const char *req, int responses, const char *want, int expect_eof)
+{
+  static reader_t r;
+  char body[256];
+  long before = atomic_load(&calls);
+  int c = client();
+  if (c < 0)
+    return;
+  r.len = 0;
+  r.eof = 0;
+  if (req)
+    send_all(c, req, strlen(req));
+  int got = 0;
+  for (int i = 0; i < responses; i++)
+  {
+    int code = read_response(c, &r, body, sizeof body);
+    if (code != 200)
+      break;
+    CHECK(!want || strcmp(body, want) == 0, "%s: body '%s', want '%s'", name, body, want);
+    got++;
+  }
+  CHECK(got == responses, "%s: %d responses, want %d", name, got, responses);
+  if (expect_eof)
+    CHECK(at_eof(c, &r), "%s: connection left open", name);
+  close(c);
+  usleep(20000);
+  printf("case %-22s responses %d  callbacks %ld\n", name, got, atomic_load(&calls) - before);
+  fflush(stdout);
+}
+
+static const char tfb[] = "GET /plaintext HTTP/1.1\r\nHost: tfb-server:8080\r\nAccept: text/plain\r\n"
+                          "Connection: keep-alive\r\nUser-Agent: wrk/4.2.0 (tfb-load)\r\n\r\n";
+
+typedef struct load_arg
+{
+  int   requests;
+  long  got;
+} load_arg_t;
+
+static void *load_client(void *p)
+{
+  load_arg_t *a = p;
+  static __thread reader_t r;
+  char body[64];
+  int c = client();
+  if (c < 0)
+    return NULL;
+  r.len = 0;
+  r.eof = 0;
+  size_t one = strlen(tfb);
+  char *req = malloc(one * (size_t) a->requests);
+  for (int i = 0; i < a->requests; i++)
+    memcpy(req + one * (size_t) i, tfb, one);
+  send_all(c, req, one * (size_t) a->requests);
+  for (int i = 0; i < a->requests; i++)
+    if (read_response(c, &r, body, sizeof body) == 200 && strcmp(body, "ok") == 0)
+      a->got++;
+  free(req);
+  close(c);
+  return NULL;
+}
+
+static int conns = 32, per_conn = 64;
+
+static void *client_main(void *unused)
+{
+  (void) unused;
+  /* the reference's cases (test/server.c:150-160) */
+  run_case("get", "GET / HTTP/1.0\r\n\r\n", 1, "ok", 0);
+  run_case("get+partial", "GET / HTTP/1.0\r\n\r\nGET", 1, "ok", 0);
+  run_case("abort", "GET /abort HTTP/1.0\r\n\r\n", 0, NULL, 1);   /* closed before the reply is flushed, as the reference */
+  run_case("next1", "GET /next1 HTTP/1.0\r\n\r\n", 1, "ok", 0);
+  run_case("next2", "GET /next2 HTTP/1.0\r\n\r\n", 1, "ok", 1);
+  run_case("next1 x2 pipelined", "GET /next1 HTTP/1.0\r\n\r\nGET /next1 HTTP/1.0\r\n\r\n", 2, "ok", 0);
+  run_case("invalid", "i n v a l i d", 0, NULL, 1);
+  run_case("connect+close", NULL, 0, NULL, 0);
+  /* BASELINE config 1: 16 pipelined 128-byte GETs in one write */
+  {
+    char req[16 * 128 + 1];
+    for (int i = 0; i < 16; i++)
+      memcpy(req + 128 * i, tfb, 128);
+    req[16 * 128] = 0;
+    CHECK(strlen(tfb) == 128, "template is %zu bytes", strlen(tfb));
+    run_case("config1 16 pipelined", req, 16, "ok", 0);
+  }
+  /* bodies: Content-Length, chunked (de-framed in place), a GET behind them */
+  run_case("post content-length", "POST /body HTTP/1.1\r\nContent-Length: 5\r\n\r\nhelloGET / HTTP/1.1\r\n\r\n", 2, NULL, 0);
+  run_case("post chunked", "POST /body HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n5\r\nhello\r\n6\r\n world\r\n0\r\n\r\n",
+           1, "hello world", 0);
+  run_case("lf line ends x2", "GET / HTTP/1.1\n\nGET / HTTP/1.1\n\n", 2, "ok", 0);
+  /* load: many connections, pipelined */
+  {
+    pthread_t t[256];
+    load_arg_t a[256];
+    int n = conns < 256 ? conns : 256;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < n; i++)
+    {
+      a[i] = (load_arg_t) {.requests = per_conn};
+      pthread_create(&t[i], NULL, load_client, &a[i]);
+    }
+    long total = 0;
+    for (int i = 0; i < n; i++)
+    {
+      pthread_join(t[i], NULL);
+      total += a[i].got;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    double s = (double) (t1.tv_sec - t0.tv_sec) + (double) (t1.tv_nsec - t0.tv_nsec) * 1e-9;
+    CHECK(total == (long) n * per_conn, "load: %ld responses, want %ld", total, (long) n * per_conn);
+    printf("load %d connections x %d pipelined: %ld responses in %.3f s (%.0f req/s)\n", n, per_conn, total, s,
+           (double) total / s);
+  }
+  if (write(stop_pipe[1], "x", 1) != 1)
+    abort();
+  return NULL;
+}
+
+int main(int argc, char **argv)
+{
+  if (argc > 1)
+    conns = atoi(argv[1]);
+  if (argc > 2)
+    per_conn = atoi(argv[2]);
+  struct sockaddr_in sin = {.sin_family = AF_INET, .sin_addr.s_addr = htonl(0x7f000001)};
+  socklen_t len = sizeof sin;
+  int s = socket(AF_INET, SOCK_STREAM, 0);
+  (void) setsockopt(s, SOL_SOCKET, SO_REUSEADDR, (int[]) {1}, sizeof(int));
+  if (bind(s, (struct sockaddr *) &sin, sizeof sin) != 0 || listen(s, 4096) != 0 ||
+      getsockname(s, (struct sockaddr *) &sin, &len) != 0)
+    return 2;
+  port = ntohs(sin.sin_port);
+  if (pipe(stop_pipe) != 0)
+    return 2;
+
+  reactor_construct();
+  server_construct(&server, server_callback, NULL);
+  server_open_socket(&server, s);
+  reactor_t stop = reactor_poll(stop_ready, &stop, stop_pipe[0], EPOLLIN);
+  printf("parser: %s\n", reactor_parser_name());
+  pthread_t t;
+  pthread_create(&t, NULL, client_main, NULL);
+  reactor_loop();
+  pthread_join(t, NULL);
+  reactor_destruct();
+  close(s);
+  printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);
+  return failures != 0;
+}

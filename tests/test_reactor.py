@@ -1,0 +1,76 @@
+"""The libreactor surface (include/reactor.h, libreactorng_amd/libreactor.so):
+the reference's example/server.c links against it unchanged, the http module
+meets the reference's test/http.c expectations, and the HTTP server serves the
+reference's test/server.c cases, BASELINE config 1 (16 pipelined 128-byte GETs)
+and a pipelined many-connection load -- with the host parser on CPU and with
+the MI355X batch parser on the GPU."""
+import json
+import os
+import re
+import struct
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "libreactorng_amd")
+BIN = os.path.join(LIB, "bin")
+REF_EXAMPLE = "/root/reference/example/server.c"
+
+
+def _vectors(tmp_path):
+    """tests/golden/http_request_tests.json (test/http.c:21-119) as the binary fixture http_test reads."""
+    v = json.load(open(os.path.join(ROOT, "tests", "golden", "http_request_tests.json")))["vectors"]
+    path = tmp_path / "vectors.bin"
+    with open(path, "wb") as f:
+        for x in v:
+            b = x["request"].encode("latin-1")
+            f.write(struct.pack("<I", len(b)) + b + struct.pack("<iI", x["result"], x["remaining"]))
+    return str(path)
+
+
+def _run(args, parser, timeout=120):
+    env = dict(os.environ, RHP_REACTOR_PARSER=parser)
+    p = subprocess.run(args, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stdout + p.stderr
+    return p.stdout
+
+
+def test_reactor_exports_every_declared_function():
+    text = open(os.path.join(ROOT, "include", "reactor.h")).read()
+    decl = set(re.findall(r"^(?!typedef)[a-z_0-9]+\s*\*?\s*([a-z_0-9]+)\s*\(", text, re.M))
+    out = subprocess.check_output(["nm", "-D", "--defined-only", os.path.join(LIB, "libreactor.so")], text=True)
+    have = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert not sorted(decl - have)
+
+
+@pytest.mark.skipif(not os.path.exists(REF_EXAMPLE), reason="reference checkout not present (dev container only)")
+def test_reference_example_server_links_unchanged(tmp_path):
+    """example/server.c of the reference, compiled and linked as it is."""
+    exe = tmp_path / "server"
+    subprocess.check_call(["gcc", "-std=gnu2x", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), REF_EXAMPLE,
+                           "-o", str(exe), "-L", LIB, "-lreactor", f"-Wl,-rpath,{LIB}"])
+    undefined = subprocess.check_output(["nm", "-u", str(exe)], text=True)
+    used = {s for s in re.findall(r"U (\w+)", undefined) if not s.startswith("__")}
+    assert {"reactor_construct", "reactor_loop", "reactor_destruct", "server_construct", "server_open",
+            "server_plain", "string"} <= used
+
+
+def test_http_module_reference_vectors(tmp_path):
+    out = _run([os.path.join(BIN, "http_test"), _vectors(tmp_path)], "host")
+    assert "read_request: 21 vectors" in out and "OK (0 failures)" in out
+
+
+def test_server_cases_host_parser():
+    out = _run([os.path.join(BIN, "server_test"), "16", "32"], "host")
+    assert "parser: host" in out and "OK (0 failures)" in out
+    assert "config1 16 pipelined   responses 16  callbacks 16" in out
+
+
+@pytest.mark.gpu
+def test_server_cases_gpu_batch_parser():
+    """The same cases with sessions parsed by rhp_parse_batch on the MI355X."""
+    out = _run([os.path.join(BIN, "server_test"), "64", "64"], "gpu")
+    print(out)
+    assert "parser: gpu" in out and "OK (0 failures)" in out
+    assert "config1 16 pipelined   responses 16  callbacks 16" in out

@@ -40,7 +40,24 @@ namespace {
 
 using namespace rhp;
 
-__device__ const Table2 g_table2 = make_table2();
+#ifndef RHP_PAIR
+#define RHP_PAIR 1   /* 1: pair DFA (rhp_dfa.h Table2), 0: byte DFA (Table8) */
+#endif
+#if RHP_PAIR
+__device__ const Table2 g_table = make_table2();
+#define kTableBytes kTable2Bytes
+__device__ __forceinline__ constexpr uint32_t start_index(uint32_t s) { return idx2(s, 0); }
+__device__ __forceinline__ bool t_slow(uint32_t i) { return is_slow2(i); }
+__device__ __forceinline__ bool t_done(uint32_t i) { return is_done2(i); }
+__device__ __forceinline__ bool t_err(uint32_t i) { return is_err2(i); }
+#else
+__device__ const Table8 g_table = make_table8();
+#define kTableBytes kTable8Bytes
+__device__ __forceinline__ constexpr uint32_t start_index(uint32_t s) { return idx8(s); }
+__device__ __forceinline__ bool t_slow(uint32_t i) { return is_slow8(i); }
+__device__ __forceinline__ bool t_done(uint32_t i) { return is_done8(i); }
+__device__ __forceinline__ bool t_err(uint32_t i) { return is_err8(i); }
+#endif
 
 struct Params {
   const uint8_t *bytes;
@@ -64,14 +81,14 @@ enum : uint32_t {
   kBlock = RHP_BLOCK,                            /* window bytes per lane per loop iteration (64 or 128) */
   kParts = kBlock / 16,                          /* 16-byte parts per window */
   kEvWords = kBlock / 32,                        /* 32-bit event words per block */
-  kLdsTable = (kTable2Bytes + 1023u) & ~1023u,  /* staging starts 1 KiB aligned */
+  kLdsTable = (kTableBytes + 1023u) & ~1023u,   /* staging starts 1 KiB aligned */
   kStageWave = 64 * kBlock,                      /* one window per lane, single-buffered */
-  kPark = 0,                                     /* idx2(S_DONE, 0): idle lanes step here */
+  kPark = 0,                                     /* the DONE index: idle lanes step here */
   kDeferExact = 0x8000u,                         /* reqs[i].flags while deferred (kernel-internal) */
   kDeferFrame = 0x4000u
 };
 static_assert(kBlock == 64 || kBlock == 128, "64- or 128-byte windows");
-static_assert(idx2(S_DONE, 0) == kPark, "parked lanes sit in DONE");
+static_assert(idx2(S_DONE, 0) == kPark && idx8(S_DONE) == kPark, "parked lanes sit in DONE");
 
 /* LDS byte address of part q (16 B) of lane w's window inside the staging
  * buffer.  The LDS-DMA loads of a wave write lane-linearly (1 KiB per
@@ -212,9 +229,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #endif
 
   {
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(&g_table2);
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(&g_table);
     u32x4 *dst = reinterpret_cast<u32x4 *>(lds);
-    for (uint32_t k = tid; k < kTable2Bytes / 16; k += WAVES * 64) dst[k] = src[k];
+    for (uint32_t k = tid; k < kTableBytes / 16; k += WAVES * 64) dst[k] = src[k];
     if (tid < 2) reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave)[tid] = 0;   /* pool counter, replay flag */
   }
   __syncthreads();
@@ -237,7 +254,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   const uint8_t *wbytes = p.bytes + base;
 
   /* ---- lane state ---- */
-  uint32_t st = kPark;                 /* pair index (rhp_dfa.h idx2) */
+  uint32_t st = kPark;                 /* table index (rhp_dfa.h idx2 / idx8) */
   int32_t pos = 0;                     /* request-relative position of the next byte to step */
   uint32_t ev[kEvWords];               /* events of the block just stepped (32 bytes per word) */
 #pragma unroll
@@ -318,6 +335,23 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     }
   };
 
+  /* a header line whose colon (CO) and end (EOL) are both in the same half
+   * block, for the lanes with `valid`: both events at once, leaving the history
+   * as the two single events would (h01 = CO, LF; e2 = the previous LF) */
+  auto header_pair = [&](bool valid, uint32_t co, uint32_t lf, rhp_hdr_t *hout) {
+    if (valid) {
+      const uint32_t prev = h01 & 0xffffu;
+      const uint32_t lo = (prev + 1u) | ((co - prev - 1u) << 16);
+      const uint32_t hi = (co + 2u) | ((lf - co - 3u) << 16);
+      hx = (hx & 0xffff0000u) | prev;
+      h01 = (co << 16) | lf;
+      kn += 256u;
+      const uint32_t nh = kn >> 8;   /* <= maxh: the pair path is only taken below the capacity */
+      if (nh & 1u) { rec_lo = lo; rec_hi = hi; }
+      else store_pair(hout + nh - 2u, u32x4{rec_lo, rec_hi, lo, hi});
+    }
+  };
+
   /*
    * Decode the block's events and finalize cur when its outcome is known
    * (decisions mirrored by rhp_emu.cpp):
@@ -328,8 +362,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   auto decode = [&]() {
     if (!has) return;
     const uint32_t e = st;
-    const bool slow = is_slow2(e);
-    const bool term_ev = is_done2(e) || is_err2(e);
+    const bool slow = t_slow(e);
+    const bool term_ev = t_done(e) || t_err(e);
     const int32_t block_pos = pos - (int32_t) kBlock;
     uint64_t mh[kEvWords / 2];
 #pragma unroll
@@ -351,11 +385,16 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #pragma unroll
     for (int h = 0; h < (int) kEvWords / 2; h++) {
       uint64_t m = (hx >> 16) ? 0ull : mh[h];
+      const uint32_t base = (uint32_t) (block_pos + 64 * h);
       while (__ballot(m != 0)) {
-        const bool valid = m != 0;
-        const uint32_t bt = (uint32_t) __builtin_ctzll(m | (1ull << 63));
-        m &= m - 1u;
-        event(valid, (uint32_t) (block_pos + 64 * h + (int32_t) bt), hout);
+        const uint32_t b0 = (uint32_t) __builtin_ctzll(m | (1ull << 63));
+        const uint64_t m1 = m & (m - 1u);
+        const uint32_t b1 = (uint32_t) __builtin_ctzll(m1 | (1ull << 63));
+        /* CO then EOL, and the line's max_headers check cannot fire */
+        const bool pair = m1 != 0 && (kn & 7u) == 3u && (kn >> 8) != maxh;
+        header_pair(pair, base + b0, base + b1, hout);
+        event(m != 0 && !pair, base + b0, hout);
+        m = pair ? (m1 & (m1 - 1u)) : m1;
         m = (hx >> 16) ? 0ull : m;
       }
     }
@@ -363,8 +402,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const bool ovf = ovf_at != 0;
     const bool fin = ovf || slow || term_ev || (uint32_t) pos >= cur_len;
     if (!fin) return;
-    const bool ok = !ovf && is_done2(e) && term_pos < cur_len;
-    const bool bad = ovf ? ovf_at - 1u < cur_len : (is_err2(e) && term_pos < cur_len);
+    const bool ok = !ovf && t_done(e) && term_pos < cur_len;
+    const bool bad = ovf ? ovf_at - 1u < cur_len : (t_err(e) && term_pos < cur_len);
     rhp_req_t r = {};
     r.minor_version = -1;
     if (ok) {
@@ -418,6 +457,24 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   };
   /* a window's 16-byte chunks: the class reads of chunk q+1 are issued before
    * the chained steps of chunk q, so their latency hides behind the chain */
+#if !RHP_PAIR
+  /* byte DFA: 16 chained steps per chunk, one event bit each */
+  auto steps_chunks = [&](const u32x4 *Wc, int nchunks, uint32_t *evw) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      if (q >= nchunks) break;
+#pragma unroll
+      for (int d = 0; d < 4; d++) {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          st = lds_u8(__builtin_amdgcn_perm(st, Wc[q][d], 0x0c0c0400u | (uint32_t) b));
+          asm("v_alignbit_b32 %0, %1, %0, 1" : "+v"(evw[q >> 1]) : "v"(st));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+#else
   auto steps_chunks = [&](const u32x4 *Wc, int nchunks, uint32_t *evw) {
     uint32_t k[16], pc[4];
     classes16(Wc[0], k);
@@ -432,24 +489,29 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (q + 1 < nchunks) codes(k, pc);
     }
   };
+#endif
 
   /* LDS-DMA of every lane's next window (nw) into the staging buffer:
    * kParts loads of 1 KiB (see stage_off) */
-  auto issue_one = [&](int i) {
-    const uint32_t src = (nw & 3u) ? (nw & ~3u) : 0xffffffffu;
-    const uint32_t w = dma_window((uint32_t) i, lane);
-    const uint32_t part = dma_part(w, lane);
-    uint32_t a = (uint32_t) __shfl((int) src, (int) w);
-#ifdef RHP_EXP_HOTWIN   /* timing experiment (config 2 only): every request reads its range's first request */
-    if (a != 0xffffffffu) a &= 255u;
-#endif
-    if (a != 0xffffffffu)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(wbytes + a + 16u * part),
-                                       (__attribute__((address_space(3))) void *) (lds + stage + 1024u * i), 16, 0, 0);
-  };
   auto issue = [&]() {
+    /* all shuffles first (one LDS round trip for the lot), then the loads; a
+     * lane without a next window fetches the range's first bytes instead (its
+     * staging slot is not read), so no load needs a branch */
+    const uint32_t src = (nw & 3u) ? (nw & ~3u) : 0u;
+    uint32_t a[kParts];
 #pragma unroll
-    for (int i = 0; i < (int) kParts; i++) issue_one(i);
+    for (int i = 0; i < (int) kParts; i++) {
+      a[i] = (uint32_t) __shfl((int) src, (int) dma_window((uint32_t) i, lane));
+#ifdef RHP_EXP_HOTWIN   /* timing experiment (config 2 only): every request reads its range's first request */
+      a[i] &= 255u;
+#endif
+    }
+#pragma unroll
+    for (int i = 0; i < (int) kParts; i++) {
+      const uint32_t part = dma_part(dma_window((uint32_t) i, lane), lane);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(wbytes + a[i] + 16u * part),
+                                       (__attribute__((address_space(3))) void *) (lds + stage + 1024u * i), 16, 0, 0);
+    }
   };
 
   refill_pend();
@@ -492,7 +554,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const uint32_t mis = (uint32_t) p_o0 & 3u;
       uint32_t s0 = mis == 0 ? S_METHOD0 : mis == 1 ? S_SKIP1 : mis == 2 ? S_SKIP2 : S_SKIP3;
       if (cur_len > kFastMaxLen) s0 = S_SLOW;
-      st = idx2(s0, 0);
+      st = start_index(s0);
       pos = -(int32_t) mis;
       h01 = hx = kn = rl = 0;
     }

@@ -30,8 +30,9 @@ __global__ void k(uint32_t *out, int iters, uint32_t seed)
       uint32_t r;
       if (PAT == 0) r = ((x >> 8) % 48u) * 256u + (x >> 24);
       else if (PAT == 1) r = 7u * 256u + (x >> 24);
-      else if (PAT == 2) r = 7u * 256u + (uint32_t) j * 4u;
-      else r = lane * 4u + (uint32_t) j * 256u;
+      else if (PAT == 4) r = 7u * 256u + 0x30u + ((x >> 24) & 0x3fu);                            /* one row, ASCII: no conflicts */
+      else if (PAT == 2) r = 7u * 256u + (((uint32_t) it * 8u + (uint32_t) j) & 63u) * 4u;   /* all lanes one address */
+      else r = (lane * W + ((uint32_t) it * 8u + (uint32_t) j) * 256u) & 0xbfffu;            /* lane-linear, conflict-free */
       a[j] = r & ~(uint32_t) (W - 1);
     }
 #pragma unroll
@@ -85,5 +86,7 @@ int main()
   run<4, 3>(d_out, cus, "lane-linear");
   run<8, 0>(d_out, cus, "random row, random byte");
   run<8, 3>(d_out, cus, "lane-linear");
+  run<1, 4>(d_out, cus, "one row, ascii byte");
+  run<4, 4>(d_out, cus, "one row, ascii byte");
   return 0;
 }

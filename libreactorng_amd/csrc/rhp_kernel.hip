@@ -177,6 +177,13 @@ __device__ __forceinline__ void ev_shift2(uint32_t &ev, uint32_t idx)
   asm("v_alignbit_b32 %0, %1, %0, 2" : "+v"(ev) : "v"(idx));
 }
 
+/* s_waitcnt vmcnt(0) / lgkmcnt(0).  Kept as inline asm: the builtin form
+ * (which the compiler's wait insertion sees, removing its own vmcnt(0) in the
+ * request switch) measured 2 % slower on config 2 -- the kernel is bound by
+ * LDS issue, not by that wait (profiles/r01/v6) */
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 /* one byte of LDS at address a (the table is at LDS address 0) */
 __device__ __forceinline__ uint32_t lds_u8(uint32_t a)
 {
@@ -188,6 +195,25 @@ __device__ __forceinline__ void store_pair(rhp_hdr_t *dst, u32x4 v)
 {
   typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
   *GLOBAL(u32x4a4, dst) = v;
+}
+/* keep the compiler from sinking the computation of x into a branch */
+__device__ __forceinline__ void opaque(uint32_t &x) { asm("" : "+v"(x)); }
+
+/* store_pair for the lanes in `mask` (a ballot), as straight-line code: the
+ * decode loop then has no branch the compiler would structurize (which costs
+ * exec bookkeeping and register copies per event).  exec is restored before
+ * the asm ends; the trailing s_nop covers the store-data read hazard. */
+__device__ __forceinline__ void store_pair_lanes(uint64_t mask, rhp_hdr_t *dst, u32x4 v)
+{
+  uint64_t saved;
+  asm volatile("s_mov_b64 %0, exec\n\t"
+               "s_mov_b64 exec, %1\n\t"
+               "global_store_dwordx4 %2, %3, off\n\t"
+               "s_mov_b64 exec, %0\n\t"
+               "s_nop 1"
+               : "=&s"(saved)
+               : "s"(mask), "v"(dst), "v"(v)
+               : "memory");
 }
 __device__ __forceinline__ void store_one(rhp_hdr_t *dst, u32x2 v)
 {
@@ -261,15 +287,21 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
   bool has = false;                    /* cur is being parsed */
   uint32_t cur = 0, cur_len = 0, cur_ptr = 0;   /* cur_ptr: window of the block being stepped */
-  /* event decoder state of cur (rhp_dfa.h Dec, packed into four registers):
-   *   h01 = e0 | e1 << 16     the two newest event positions
-   *   hx  = e2 | ovf << 16    the third; ovf = 0, or 1 + the line start at
-   *                           which max_headers overflowed
-   *   kn  = k | minor << 3 | nh << 8   events consumed (0..2 request line,
-   *                           then 3,4 = CO, EOL), minor version, headers done
-   *   rl  = method_len | path_len << 16 */
-  uint32_t h01 = 0, hx = 0, kn = 0, rl = 0;
-  uint32_t rec_lo = 0, rec_hi = 0;     /* header record waiting for its pair */
+  /* event decoder state of cur (the records of rhp_dfa.h dec_event, built
+   * incrementally: every event at p yields part = A | (p - B) << 16):
+   *   kn  = k | minor << 3 | nh << 8   events consumed (0..2 request line:
+   *                           ME, PE, RL; then 3,4 = CO, EOL), minor version,
+   *                           headers done
+   *   A,B the anchors of the next event: at PE (A, B) = (ME, ME + 1), so part
+   *       = the request-line record; at CO (line start, line start), so part
+   *       = name_off | name_len << 16; at EOL (CO + 2, CO + 3), so part =
+   *       value_off | value_len << 16
+   *   ovf = 0, or 1 + the line start at which max_headers overflowed
+   *   rl  = method_len | path_len << 16
+   *   cur_lo: name part of the line in progress; rec_lo/rec_hi: the odd
+   *   header record waiting for its pair (16-byte stores) */
+  uint32_t kn = 0, A = 0, B = 0, ovf = 0, rl = 0, cur_lo = 0;
+  uint32_t rec_lo = 0, rec_hi = 0;
   bool pend_ok = false;                /* pend: the lane's next request */
   uint32_t pend = 0;
   uint32_t pend_o0 = 0, pend_o1 = 0;   /* low dwords of offsets[pend], offsets[pend+1] as loaded */
@@ -303,53 +335,63 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     }
   };
 
-  /* one non-terminal event at request position ep, for the lanes with `valid`
-   * (rhp_dfa.h dec_event): the history shift and the event counter are
-   * straight-line; the request-line record (once per request) and the header
-   * record (every second event) are branches taken only by the lanes concerned */
-  auto event = [&](bool valid, uint32_t ep, rhp_hdr_t *hout) {
-    const uint32_t k = kn & 7u;
-    if (valid) {
-      hx = (hx & 0xffff0000u) | (h01 >> 16);
-      h01 = (h01 << 16) | ep;
-      kn += k == 4 ? 0xffffffffu : 1u;
-      /* CO: history = CO, prevLF; the max_headers check of the line start */
-      if (k == 3 && (kn >> 8) == maxh && (hx >> 16) == 0) hx |= ((h01 >> 16) + 2u) << 16;
+  /* one non-terminal event at request position ep (rhp_dfa.h dec_event), for
+   * a lane with an event: straight-line selects, one store branch.  The
+   * max_headers check (picohttpparser.c:281-284) fires at the CO of a line
+   * that starts while nh == maxh; decoding stops there (m = 0), so nh never
+   * exceeds maxh and every completed record is stored. */
+  auto event = [&](auto &w, uint32_t base, rhp_hdr_t *hout) {
+    /* the lowest event of the mask w (lanes with w == 0 change nothing), and
+     * the next one: a header line whose CO and EOL both lie in w is taken in
+     * one iteration */
+    const bool v = w != 0;
+    auto ctz = [](auto x) -> uint32_t {
+      return (uint32_t) (sizeof(x) == 8 ? __builtin_ctzll((uint64_t) x) : __builtin_ctz((uint32_t) x));
+    };
+    const uint32_t ep = base + ctz(w);
+    auto w1 = w & (w - 1u);
+    const uint32_t ep1 = base + ctz(w1);
+    const uint32_t k = v ? kn & 7u : 7u;   /* 7: no event */
+    const uint32_t part = A | ((ep - B) << 16);
+    /* request line (once per request, so behind a uniform branch) -- ME:
+     * (A, B) = (ME, ME + 1);  PE: rl = part, A = B = the first line start
+     * (PE + 11);  RL: minor = RL - PE - 9 = ep - B + 2 */
+    if (__builtin_amdgcn_ballot_w64(k < 3u)) {
+      const bool r0 = k == 0u, r1 = k == 1u, r2 = k == 2u;
+      uint32_t a0 = ep + 1u, a1 = ep + 11u, mv = ((ep - B + 2u) & 1u) << 3;
+      opaque(a0); opaque(a1); opaque(mv);
+      rl = r1 ? part : rl;
+      kn += r2 ? mv + 1u : (r0 || r1) ? 1u : 0u;
+      A = r0 ? ep : r1 ? a1 : A;
+      B = r0 ? a0 : r1 ? a1 : B;
     }
-    if (valid && k == 2) {   /* RL: history = RL, PE, ME */
-      const uint32_t pe = h01 >> 16, me = hx & 0xffffu;
-      rl = me | ((pe - me - 1u) << 16);
-      kn |= (ep - pe - 9u) << 3;
-      h01 = (h01 & 0xffff0000u) | (pe + 10u);
+    /* header line: CO (k = 3) -> name part, anchors (CO + 2, CO + 3);
+     * EOL (k = 4) -> value part, record complete, anchors = the next line start;
+     * pair: CO and EOL of one line (below the max_headers capacity) */
+    const bool atmax = (kn >> 8) == maxh;
+    const bool pair = k == 3u && w1 != 0 && !atmax;
+    const bool co = k == 3u && !pair, eol = k == 4u;
+    if (__builtin_amdgcn_ballot_w64(co && atmax)) {   /* max_headers check at the line start: stop */
+      const bool ov = co && atmax;
+      uint32_t o = A + 1u;
+      opaque(o);
+      ovf = ov ? o : ovf;
+      w1 = ov ? 0 : w1;
     }
-    if (valid && k == 4) {   /* EOL: history = LF, CO, prevLF */
-      const uint32_t co = h01 >> 16, prev = hx & 0xffffu;
-      const uint32_t lo = (prev + 1u) | ((co - prev - 1u) << 16);
-      const uint32_t hi = (co + 2u) | ((ep - co - 3u) << 16);
-      kn += 256u;
-      const uint32_t nh = kn >> 8;
-      if (nh <= maxh) {
-        if (nh & 1u) { rec_lo = lo; rec_hi = hi; }
-        else store_pair(hout + nh - 2u, u32x4{rec_lo, rec_hi, lo, hi});
-      }
-    }
-  };
-
-  /* a header line whose colon (CO) and end (EOL) are both in the same half
-   * block, for the lanes with `valid`: both events at once, leaving the history
-   * as the two single events would (h01 = CO, LF; e2 = the previous LF) */
-  auto header_pair = [&](bool valid, uint32_t co, uint32_t lf, rhp_hdr_t *hout) {
-    if (valid) {
-      const uint32_t prev = h01 & 0xffffu;
-      const uint32_t lo = (prev + 1u) | ((co - prev - 1u) << 16);
-      const uint32_t hi = (co + 2u) | ((lf - co - 3u) << 16);
-      hx = (hx & 0xffff0000u) | prev;
-      h01 = (co << 16) | lf;
-      kn += 256u;
-      const uint32_t nh = kn >> 8;   /* <= maxh: the pair path is only taken below the capacity */
-      if (nh & 1u) { rec_lo = lo; rec_hi = hi; }
-      else store_pair(hout + nh - 2u, u32x4{rec_lo, rec_hi, lo, hi});
-    }
+    uint32_t c2 = ep + 2u, c3 = ep + 3u, e1 = ep + 1u, p1 = c2 | ((ep1 - c3) << 16), f1 = ep1 + 1u;
+    opaque(c2); opaque(c3); opaque(e1); opaque(p1); opaque(f1);
+    const bool done = pair || eol;              /* a record completes */
+    const uint32_t r_lo = pair ? part : cur_lo, r_hi = pair ? p1 : part;
+    cur_lo = co ? part : cur_lo;
+    kn += co ? 1u : eol ? 255u : pair ? 256u : 0u;
+    A = co ? c2 : eol ? e1 : pair ? f1 : A;
+    B = co ? c3 : eol ? e1 : pair ? f1 : B;
+    w = pair ? w1 & (w1 - 1u) : w1;
+    const bool odd = (kn & 256u) != 0;
+    rec_lo = done && odd ? r_lo : rec_lo;
+    rec_hi = done && odd ? r_hi : rec_hi;
+    const uint64_t st_m = __builtin_amdgcn_ballot_w64(done && !odd);
+    if (st_m) store_pair_lanes(st_m, hout + (kn >> 8) - 2u, u32x4{rec_lo, rec_hi, r_lo, r_hi});
   };
 
   /*
@@ -382,28 +424,27 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       }
     }
     rhp_hdr_t *hout = p.hdrs + (uint64_t) cur * maxh;
+#ifdef RHP_DEC32   /* 32-bit event words (experiment) */
+#pragma unroll
+    for (int q = 0; q < (int) kEvWords; q++) {
+      uint32_t w = ovf ? 0u : (uint32_t) (mh[q >> 1] >> (32 * (q & 1)));
+      const uint32_t base = (uint32_t) (block_pos + 32 * q);
+      if (__ballot(w != 0)) do event(w, base, hout); while (__ballot(w != 0));
+    }
+#else              /* 64-bit halves: fewer iterations when events are dense */
 #pragma unroll
     for (int h = 0; h < (int) kEvWords / 2; h++) {
-      uint64_t m = (hx >> 16) ? 0ull : mh[h];
+      uint64_t w = ovf ? 0ull : mh[h];
       const uint32_t base = (uint32_t) (block_pos + 64 * h);
-      while (__ballot(m != 0)) {
-        const uint32_t b0 = (uint32_t) __builtin_ctzll(m | (1ull << 63));
-        const uint64_t m1 = m & (m - 1u);
-        const uint32_t b1 = (uint32_t) __builtin_ctzll(m1 | (1ull << 63));
-        /* CO then EOL, and the line's max_headers check cannot fire */
-        const bool pair = m1 != 0 && (kn & 7u) == 3u && (kn >> 8) != maxh;
-        header_pair(pair, base + b0, base + b1, hout);
-        event(m != 0 && !pair, base + b0, hout);
-        m = pair ? (m1 & (m1 - 1u)) : m1;
-        m = (hx >> 16) ? 0ull : m;
-      }
+      if (__ballot(w != 0)) do event(w, base, hout); while (__ballot(w != 0));
     }
-    const uint32_t ovf_at = hx >> 16;
-    const bool ovf = ovf_at != 0;
-    const bool fin = ovf || slow || term_ev || (uint32_t) pos >= cur_len;
+#endif
+    const uint32_t ovf_at = ovf;
+    const bool ovfl = ovf_at != 0;
+    const bool fin = ovfl || slow || term_ev || (uint32_t) pos >= cur_len;
     if (!fin) return;
-    const bool ok = !ovf && t_done(e) && term_pos < cur_len;
-    const bool bad = ovf ? ovf_at - 1u < cur_len : (t_err(e) && term_pos < cur_len);
+    const bool ok = !ovfl && t_done(e) && term_pos < cur_len;
+    const bool bad = ovfl ? ovf_at - 1u < cur_len : (t_err(e) && term_pos < cur_len);
     rhp_req_t r = {};
     r.minor_version = -1;
     if (ok) {
@@ -531,8 +572,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   for (;;) {
     RHP_STAMP(t0);
     /* [A] */
+    wait_vm0();   /* the window's LDS-DMA has landed (and the pending offsets) */
     const uint32_t p_o0 = pend_o0, p_o1 = pend_o1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* the window's LDS-DMA has landed */
 #pragma unroll
     for (int q = 0; q < kWRegs; q++) W[q] = *reinterpret_cast<const u32x4 *>(lds + stage + stage_off(lane, q));
 #ifdef RHP_STAMPS
@@ -556,7 +597,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (cur_len > kFastMaxLen) s0 = S_SLOW;
       st = start_index(s0);
       pos = -(int32_t) mis;
-      h01 = hx = kn = rl = 0;
+      kn = A = B = ovf = rl = 0;
     }
     if (nw_kind) cur_ptr = nw & ~3u;
     const bool pend_ready = pend_ok;   /* assigned before this block: p_o0/p_o1 valid */
@@ -569,7 +610,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     nw = 0;
     if (has && (uint32_t) (pos + (int32_t) kBlock) < cur_len) nw = (cur_ptr + kBlock) | 1u;
     else if (pend_ready) nw = ((p_o0 & ~3u) - (uint32_t) base) | 2u;
-    if (kBlock == 128) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   /* [A]'s reads of the buffer are done */
+    if (kBlock == 128) wait_lgkm0();   /* [A]'s reads of the buffer are done */
     if (kBlock == 128) issue();
     if (!__ballot(has || nw || pend_ok)) break;
 #ifdef RHP_STAMPS
@@ -586,14 +627,17 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #endif
 #pragma unroll
       for (int q = 0; q < 2; q++) W[q] = *reinterpret_cast<const u32x4 *>(lds + stage + stage_off(lane, q + 2));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   /* the buffer is read: refill it */
+      wait_lgkm0();   /* the buffer is read: refill it */
       issue();
 #ifndef RHP_EXP_NOSTEP
       steps_chunks(W, 2, ev + 1);
 #endif
     } else {
 #ifndef RHP_EXP_NOSTEP
-      steps_chunks(W, 8, ev);
+      /* no lane has a request (the first iteration of every wave, whose
+       * windows are still in flight): skip the walk, which would only step
+       * parked lanes through the LDS */
+      if (__builtin_amdgcn_ballot_w64(has)) steps_chunks(W, 8, ev);
 #endif
     }
     pos += (int32_t) kBlock;

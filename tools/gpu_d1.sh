@@ -1,0 +1,4 @@
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}" && mkdir -p gpurun_out && export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_d1.log 2>&1 && echo PYTEST_OK || { tail -40 gpurun_out/pytest_d1.log; exit 1; }
+TAG=d1 LIBS_WAVES="librhp_base:16 librhp:16" CFGS="get256 zipf post" bash tools/exp_cfg.sh && LIBS_CFG="librhp_stamps:2 librhp_stamps:3" bash tools/stamps_ab.sh

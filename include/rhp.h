@@ -73,7 +73,7 @@ typedef struct rhp_http {
 } rhp_http_t;
 
 typedef struct rhp_batch {
-  const uint8_t  *bytes;   /* device: packed requests + RHP_PAD zero bytes */
+  const uint8_t  *bytes;   /* device, 16-byte aligned: packed requests + RHP_PAD zero bytes */
   uint8_t        *bytes_rw;/* device, RHP_MODE_HTTP: same buffer, writable (chunked
                               bodies are de-framed in place, http.c:134-160); may be NULL
                               in RHP_MODE_PHR */

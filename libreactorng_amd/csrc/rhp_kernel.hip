@@ -129,6 +129,29 @@ __device__ unsigned long long g_stamps[8192 * 8];
 #define RHP_STAMP(t) do { } while (0)
 #endif
 
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+/* The exact parser's byte reader on the GPU: the aligned 16-byte line holding
+ * the last byte read stays in registers, so its sequential scan makes one
+ * global load per 16 bytes (the batch buffer is 16-aligned and padded) */
+struct LineBytes {
+  const uint8_t *b;
+  uint64_t line;
+  u32x4_t c;
+  __device__ uint32_t operator()(uint64_t p)
+  {
+    const uint64_t a = (uint64_t) (uintptr_t) b + p;
+    const uint64_t l = a & ~(uint64_t) 15;
+    if (l != line) {
+      c = *reinterpret_cast<const __attribute__((address_space(1))) u32x4_t *>((uintptr_t) l);
+      line = l;
+    }
+    const uint32_t q = (uint32_t) (a >> 2) & 3u;
+    const uint32_t d = q == 0 ? c[0] : q == 1 ? c[1] : q == 2 ? c[2] : c[3];
+    return (d >> (8u * ((uint32_t) a & 3u))) & 0xffu;
+  }
+};
+
 /* Exact scalar path for one request (phr or http mode).  Only called from the
  * post-loop replay, where inlining it lets it reuse the loop's dead registers. */
 __device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64_t off, uint64_t len)
@@ -149,18 +172,24 @@ __device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64
   }
   if (p.mode == RHP_MODE_HTTP) {
     rhp_http_t x;
-    scalar_http(p.bytes_rw + off, len, p.max_headers, &r, h, &x);
+    LineBytes B{p.bytes_rw + off, ~0ull, {0, 0, 0, 0}};
+    scalar_http_t(B, p.bytes_rw + off, len, p.max_headers, &r, h, &x);
     p.http[i] = x;
   } else {
-    scalar_phr(p.bytes + off, len, p.max_headers, &r, h);
+    LineBytes B{p.bytes + off, ~0ull, {0, 0, 0, 0}};
+    scalar_phr_t(B, len, p.max_headers, &r, h);
   }
   p.reqs[i] = r;
 }
 
 /* http_read_request framing of a request the DFA parsed (http mode only) */
-__device__ __forceinline__ void finish_http(const Params &p, uint32_t i, uint64_t off, uint64_t len, rhp_req_t r)
+__device__ __forceinline__ void finish_http(const Params &p, uint32_t i, uint64_t off, uint64_t len, rhp_req_t r,
+                                            uint32_t cand)
 {
-  http_frame(p.bytes_rw + off, len, r, p.hdrs + (uint64_t) i * p.max_headers, &p.http[i]);
+  /* cand: the framing candidates the decode left in http[i].consumed (bit 31:
+   * more than 31 headers, check all) */
+  http_frame(p.bytes_rw + off, len, r, p.hdrs + (uint64_t) i * p.max_headers, &p.http[i],
+             (cand >> 31) ? ~0ull : (uint64_t) cand);
 }
 
 /* Params pointers are generic in the kernel's view (they sit in a struct);
@@ -301,6 +330,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    *   cur_lo: name part of the line in progress; rec_lo/rec_hi: the odd
    *   header record waiting for its pair (16-byte stores) */
   uint32_t kn = 0, A = 0, B = 0, ovf = 0, rl = 0, cur_lo = 0;
+  uint32_t cand = 0;                   /* http mode: headers whose name length is 14 or 17 (bit 31: index > 30) */
   uint32_t rec_lo = 0, rec_hi = 0;
   bool pend_ok = false;                /* pend: the lane's next request */
   uint32_t pend = 0;
@@ -388,6 +418,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     B = co ? c3 : eol ? e1 : pair ? f1 : B;
     w = pair ? w1 & (w1 - 1u) : w1;
     const bool odd = (kn & 256u) != 0;
+    if (p.mode == RHP_MODE_HTTP) {   /* uniform: framing candidates only in http mode */
+      const uint32_t nlen = r_lo >> 16, hidx = (kn >> 8) - 1u;
+      cand |= done && (nlen == 14u || nlen == 17u) ? (hidx < 31u ? 1u << hidx : 0x80000000u) : 0u;
+    }
     rec_lo = done && odd ? r_lo : rec_lo;
     rec_hi = done && odd ? r_hi : rec_hi;
     const uint64_t st_m = __builtin_amdgcn_ballot_w64(done && !odd);
@@ -457,7 +491,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       r.minor_version = (int8_t) ((kn >> 3) & 1u);
       r.num_headers = (uint16_t) nh;
       r.flags = p.mode == RHP_MODE_HTTP ? (uint16_t) kDeferFrame : (uint16_t) 0;   /* framing: replay */
-      if (p.mode == RHP_MODE_HTTP) *wg_deferred = 1u;
+      if (p.mode == RHP_MODE_HTTP) {
+        *wg_deferred = 1u;
+        *GLOBAL(uint64_t, &p.http[cur].consumed) = cand;   /* framing candidates for the replay */
+      }
     } else if (bad) {
       r.ret = -1;
       if (p.mode == RHP_MODE_HTTP) store_http_bad(p.http + cur);
@@ -597,7 +634,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (cur_len > kFastMaxLen) s0 = S_SLOW;
       st = start_index(s0);
       pos = -(int32_t) mis;
-      kn = A = B = ovf = rl = 0;
+      kn = A = B = ovf = rl = cand = 0;
     }
     if (nw_kind) cur_ptr = nw & ~3u;
     const bool pend_ready = pend_ok;   /* assigned before this block: p_o0/p_o1 valid */
@@ -637,7 +674,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       /* no lane has a request (the first iteration of every wave, whose
        * windows are still in flight): skip the walk, which would only step
        * parked lanes through the LDS */
+#ifdef RHP_WALK_ALL
       if (__builtin_amdgcn_ballot_w64(has)) steps_chunks(W, 8, ev);
+#else
+      if (has) steps_chunks(W, 8, ev);   /* idle lanes off: their LDS reads are not issued */
+#endif
 #endif
     }
     pos += (int32_t) kBlock;
@@ -666,15 +707,19 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #ifndef RHP_NO_REPLAY   /* register-pressure experiments only: deferred requests stay unfinished */
   if (*wg_deferred) {
     for (uint32_t i = wg_lo + tid; i < wg_hi; i += WAVES * 64) {
-      const uint32_t f = p.reqs[i].flags;
+      /* everything a request needs first, in one round trip */
+      rhp_req_t r;
+      const u32x4 rv = *GLOBAL(const u32x4, p.reqs + i);
+      __builtin_memcpy(&r, &rv, sizeof r);
+      const uint64_t off = p.offsets[i], end = p.offsets[i + 1];
+      const uint32_t cand = p.mode == RHP_MODE_HTTP ? (uint32_t) p.http[i].consumed : 0u;
+      const uint32_t f = r.flags;
       if (!(f & (kDeferExact | kDeferFrame))) continue;
-      const uint64_t off = p.offsets[i], len = p.offsets[i + 1] - off;
       if (f & kDeferExact) {
-        finish_exact(p, i, off, len);
+        finish_exact(p, i, off, end - off);
       } else {
-        rhp_req_t r = p.reqs[i];
         r.flags = 0;
-        finish_http(p, i, off, len, r);
+        finish_http(p, i, off, end - off, r, cand);
         p.reqs[i].flags = 0;
       }
     }
@@ -760,6 +805,7 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   if (!b) return -22;
   if (b->n == 0) return 0;                       /* nothing to parse, nothing touched */
   if (!b->bytes || !b->offsets || !b->reqs || !b->work) return -22;
+  if (((uintptr_t) b->bytes & 15u) != 0) return -22;   /* windows and exact-path lines are aligned loads */
   if (b->max_headers > RHP_MAX_HEADERS) return -22;
   if (b->max_headers > 0 && !b->hdrs) return -22;
   if (b->mode == RHP_MODE_HTTP && (!b->http || !b->bytes_rw)) return -22;

@@ -20,8 +20,10 @@
 
 #if defined(__HIPCC__)
 #define RHP_HD __host__ __device__ __forceinline__
+#define RHP_HDM __host__ __device__ __forceinline__
 #else
 #define RHP_HD static inline
+#define RHP_HDM inline
 #endif
 
 namespace rhp {
@@ -39,57 +41,66 @@ RHP_HD bool is_tchar(uint32_t c)
 RHP_HD bool is_ctl_del(uint32_t c) { return c < 0x20u || c == 0x7fu; }
 RHP_HD bool is_ows(uint32_t c) { return c == ' ' || c == '\t'; }
 
+/* Byte access for the exact parser.  PlainBytes indexes memory directly
+ * (host); the GPU replay uses a reader that caches the aligned 16-byte line
+ * holding the last byte read, so a sequential scan costs one global load per
+ * 16 bytes instead of one dependent load per byte. */
+struct PlainBytes {
+  const uint8_t *b;
+  RHP_HDM uint32_t operator()(uint64_t p) const { return b[p]; }
+};
+
 /* Parse one request.  b may be read beyond len (batch contract).  Headers are
  * written to h[0..max).  Returns the phr status; fills r. */
-RHP_HD int scalar_phr(const uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h)
+template <class Bytes>
+RHP_HD int scalar_phr_t(Bytes &B, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h)
 {
   uint64_t p = 0;
   r->method_off = 0; r->method_len = 0; r->path_off = 0; r->path_len = 0;
   r->minor_version = -1; r->num_headers = 0;
 #define RHP_FAIL(code) do { r->ret = (code); return (code); } while (0)
 #define RHP_EOF() do { if (p == len) RHP_FAIL(kPartial); } while (0)
-#define RHP_CRLF() do { ++p; RHP_EOF(); if (b[p++] != '\n') RHP_FAIL(kBad); } while (0)
+#define RHP_CRLF() do { ++p; RHP_EOF(); if (B(p++) != '\n') RHP_FAIL(kBad); } while (0)
   RHP_EOF();
-  if (b[p] == '\r') RHP_CRLF();
-  else if (b[p] == '\n') ++p;
+  if (B(p) == '\r') RHP_CRLF();
+  else if (B(p) == '\n') ++p;
 
   uint64_t tok[2][2];              /* [method, path][start, end] */
   for (int t = 0; t < 2; t++) {
     tok[t][0] = p;
     RHP_EOF();
     for (;;) {
-      uint32_t c = b[p];
+      uint32_t c = B(p);
       if (c == ' ') break;
       if (is_ctl_del(c)) RHP_FAIL(kBad);
       ++p;
       RHP_EOF();
     }
     tok[t][1] = p;
-    do ++p; while (b[p] == ' ');   /* no EOF test: may run past len */
+    do ++p; while (B(p) == ' ');   /* no EOF test: may run past len */
   }
   if (tok[0][1] == tok[0][0] || tok[1][1] == tok[1][0]) RHP_FAIL(kBad);
   if ((int64_t) len - (int64_t) p < 9) RHP_FAIL(kPartial);
-  const uint8_t *v = b + p;
-  if (v[0] != 'H' || v[1] != 'T' || v[2] != 'T' || v[3] != 'P' || v[4] != '/' || v[5] != '1' ||
-      v[6] != '.' || v[7] < '0' || v[7] > '9')
+  if (B(p) != 'H' || B(p + 1) != 'T' || B(p + 2) != 'T' || B(p + 3) != 'P' || B(p + 4) != '/' ||
+      B(p + 5) != '1' || B(p + 6) != '.' || B(p + 7) - '0' > 9u)
     RHP_FAIL(kBad);
-  int minor = v[7] - '0';
+  int minor = (int) B(p + 7) - '0';
   p += 8;
-  if (b[p] == '\r') RHP_CRLF();
-  else if (b[p] == '\n') ++p;
+  if (B(p) == '\r') RHP_CRLF();
+  else if (B(p) == '\n') ++p;
   else RHP_FAIL(kBad);
 
   uint32_t n = 0;
   for (;;) {
     RHP_EOF();
-    if (b[p] == '\r') { RHP_CRLF(); break; }
-    if (b[p] == '\n') { ++p; break; }
+    if (B(p) == '\r') { RHP_CRLF(); break; }
+    if (B(p) == '\n') { ++p; break; }
     if (n == max) RHP_FAIL(kBad);
     uint64_t name = p, name_len = 0;
-    bool fold = n != 0 && is_ows(b[p]);
+    bool fold = n != 0 && is_ows(B(p));
     if (!fold) {
       for (;;) {
-        uint32_t c = b[p];
+        uint32_t c = B(p);
         if (c == ':') break;
         if (!is_tchar(c)) RHP_FAIL(kBad);
         ++p;
@@ -100,21 +111,21 @@ RHP_HD int scalar_phr(const uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r
       ++p;
       for (;; ++p) {
         RHP_EOF();
-        if (!is_ows(b[p])) break;
+        if (!is_ows(B(p))) break;
       }
     }
     uint64_t vs = p;
     uint32_t c;
     for (;; ++p) {
       RHP_EOF();
-      c = b[p];
+      c = B(p);
       if ((c < 0x20u && c != '\t') || c == 0x7fu) break;
     }
     uint64_t ve = p;
     if (c == '\r') RHP_CRLF();
     else if (c == '\n') ++p;
     else RHP_FAIL(kBad);
-    while (ve > vs && is_ows(b[ve - 1])) --ve;
+    while (ve > vs && is_ows(B(ve - 1))) --ve;
     h[n].name_off = fold ? (uint16_t) RHP_NAME_NULL : (uint16_t) name;
     h[n].name_len = (uint16_t) name_len;
     h[n].value_off = (uint16_t) vs;
@@ -134,31 +145,59 @@ RHP_HD int scalar_phr(const uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r
   return r->ret;
 }
 
+RHP_HD int scalar_phr(const uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h)
+{
+  PlainBytes B{b};
+  return scalar_phr_t(B, len, max, r, h);
+}
+
 /* ---- http_read_request framing (http.c:177-234) over a parsed request ---- */
 
 RHP_HD uint32_t upper(uint32_t c) { return (c - 'a' < 26u) ? c - 32u : c; }
 
+/* Case-insensitive name compare.  All n bytes are read before any is tested
+ * (no early exit), so on the GPU replay path they are independent loads: one
+ * memory round trip instead of n dependent ones. */
 RHP_HD bool name_eq(const uint8_t *b, const rhp_hdr_t &h, const char *name, uint32_t n)
 {
   if (h.name_off == RHP_NAME_NULL || h.name_len != n) return false;
-  for (uint32_t i = 0; i < n; i++)
-    if (upper(b[h.name_off + i]) != upper((uint8_t) name[i])) return false;
-  return true;
+  uint32_t diff = 0;
+  for (uint32_t i = 0; i < n; i++) diff |= upper(b[h.name_off + i]) ^ upper((uint8_t) name[i]);
+  return diff == 0;
 }
 
-/* strtoull(s, NULL, 10), glibc C locale (saturating, sign-negated) */
+/* strtoull(s, NULL, 10), glibc C locale (saturating, sign-negated), as a
+ * state machine over bytes: 0 leading space, 1 digits (after an optional
+ * sign), 2 done. */
+RHP_HD void num_step(uint32_t c, uint32_t &st, bool &neg, bool &ovf, uint64_t &v)
+{
+  const bool digit = c - '0' < 10u;
+  if (st == 0) {
+    if (c == ' ' || c - '\t' < 5u) return;
+    if (c == '+' || c == '-') { neg = c == '-'; st = 1; return; }
+    st = digit ? 1u : 2u;
+  } else if (st == 1 && !digit) {
+    st = 2;
+  }
+  if (st != 1 || !digit) return;
+  const uint64_t d = c - '0';
+  ovf |= v > (~0ull - d) / 10;
+  v = v * 10 + d;
+}
+
+/* The first kNumWindow bytes are read up front (independent loads); the
+ * byte walk continues past them only for longer inputs.  Reading ahead stays
+ * inside the request buffer and its RHP_PAD zero tail. */
 RHP_HD uint64_t strtoull10(const uint8_t *s)
 {
-  while (*s == ' ' || (*s >= '\t' && *s <= '\r')) s++;
-  bool neg = false;
-  if (*s == '+' || *s == '-') neg = *s++ == '-';
+  constexpr int kNumWindow = 24;
+  uint32_t w[kNumWindow];
+  for (int i = 0; i < kNumWindow; i++) w[i] = s[i];
+  uint32_t st = 0;
+  bool neg = false, ovf = false;
   uint64_t v = 0;
-  bool ovf = false;
-  for (; *s >= '0' && *s <= '9'; s++) {
-    uint64_t d = *s - '0';
-    ovf |= v > (~0ull - d) / 10;
-    v = v * 10 + d;
-  }
+  for (int i = 0; i < kNumWindow; i++) num_step(w[i], st, neg, ovf, v);
+  for (const uint8_t *q = s + kNumWindow; st != 2; q++) num_step(*q, st, neg, ovf, v);
   return ovf ? ~0ull : neg ? 0 - v : v;
 }
 
@@ -229,30 +268,52 @@ RHP_HD int64_t dechunk(uint8_t *in, uint64_t size, uint64_t *body_len)
 }
 
 /* Framing decision given a successful phr parse (n = r.ret > 0). */
-RHP_HD void http_frame(uint8_t *b, uint64_t len, const rhp_req_t &r, const rhp_hdr_t *h, rhp_http_t *x)
+/* cand: the header indices whose name could be Transfer-Encoding or
+ * Content-Length (name length 17 or 14), as found by the kernel's decode; ~0
+ * checks every header */
+RHP_HD void http_frame(uint8_t *b, uint64_t len, const rhp_req_t &r, const rhp_hdr_t *h, rhp_http_t *x,
+                       uint64_t cand = ~0ull)
 {
   const int64_t n = r.ret;
+  /* one framing candidate (the common case): its record is read together
+   * with the method bytes, and its name together with its value digits, so
+   * the GPU replay makes two memory round trips here instead of five */
+  const bool one = cand != 0 && (cand & (cand - 1)) == 0;
+  const uint32_t c = one ? (uint32_t) __builtin_ctzll(cand) : 0u;
+  rhp_hdr_t hc = {0, 0, 0, 0};
+  if (one && c < r.num_headers) hc = h[c];
+  const bool get = r.method_len == 3 && ((b[r.method_off] == 'G') & (b[r.method_off + 1] == 'E') & (b[r.method_off + 2] == 'T'));
   x->result = 1; x->body_kind = 0; x->consumed = (uint64_t) n; x->body_len = 0;
-  if (r.method_len == 3 && b[r.method_off] == 'G' && b[r.method_off + 1] == 'E' && b[r.method_off + 2] == 'T')
-    return;                                       /* GET fast path (http.c:198-202) */
+  if (get) return;                                /* GET fast path (http.c:198-202) */
   int te = -1, cl = -1;
-  for (uint32_t i = 0; i < r.num_headers; i++) {
-    if (te < 0 && name_eq(b, h[i], "Transfer-Encoding", 17)) te = (int) i;
-    if (cl < 0 && name_eq(b, h[i], "Content-Length", 14)) cl = (int) i;
+  uint64_t size = 0;
+  if (one) {
+    if (c < r.num_headers) {
+      size = hc.value_len ? strtoull10(b + hc.value_off) : 0;   /* used only if the name is Content-Length */
+      if (name_eq(b, hc, "Transfer-Encoding", 17)) te = (int) c;
+      if (name_eq(b, hc, "Content-Length", 14)) cl = (int) c;
+    }
+  } else {
+    for (uint32_t i = 0; i < r.num_headers; i++) {
+      if (i < 64 && !((cand >> i) & 1u)) continue;
+      if (te < 0 && name_eq(b, h[i], "Transfer-Encoding", 17)) te = (int) i;
+      if (cl < 0 && name_eq(b, h[i], "Content-Length", 14)) cl = (int) i;
+    }
+    if (cl >= 0 && h[cl].value_len != 0) size = strtoull10(b + h[cl].value_off);
   }
-  bool te_set = te >= 0 && h[te].value_len != 0;
-  bool cl_set = cl >= 0 && h[cl].value_len != 0;
+  const bool te_set = te >= 0 && (one ? hc.value_len : h[te].value_len) != 0;
+  const bool cl_set = cl >= 0 && (one ? hc.value_len : h[cl].value_len) != 0;
   if (cl_set) {
     if (te_set) { x->result = -1; x->consumed = 0; return; }
-    uint64_t size = strtoull10(b + h[cl].value_off);
     if (len < (uint64_t) n + size) { x->result = 0; x->consumed = 0; return; }
     x->body_kind = 1; x->body_len = size; x->consumed = (uint64_t) n + size;
     return;
   }
   if (te_set) {
     const char *ch = "CHUNKED";
-    bool eq = h[te].value_len == 7;
-    for (uint32_t i = 0; eq && i < 7; i++) eq = upper(b[h[te].value_off + i]) == (uint32_t) ch[i];
+    uint32_t diff = h[te].value_len ^ 7u;
+    for (uint32_t i = 0; i < 7; i++) diff |= upper(b[h[te].value_off + i]) ^ (uint32_t) ch[i];
+    const bool eq = diff == 0;
     if (!eq) { x->result = -1; x->consumed = 0; return; }
     uint64_t blen = 0;
     int64_t size = dechunk(b + n, len - (uint64_t) n, &blen);
@@ -262,13 +323,19 @@ RHP_HD void http_frame(uint8_t *b, uint64_t len, const rhp_req_t &r, const rhp_h
 }
 
 /* Whole http_read_request for one request. */
-RHP_HD void scalar_http(uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, rhp_http_t *x)
+template <class Bytes>
+RHP_HD void scalar_http_t(Bytes &B, uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, rhp_http_t *x)
 {
-  int n = scalar_phr(b, len, max, r, h);
+  int n = scalar_phr_t(B, len, max, r, h);
   x->body_kind = 0; x->consumed = 0; x->body_len = 0;
   if (len == 0) { x->result = 0; return; }
   if (n <= 0) { x->result = n == kBad ? -1 : 0; return; }
   http_frame(b, len, *r, h, x);
+}
+RHP_HD void scalar_http(uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, rhp_http_t *x)
+{
+  PlainBytes B{b};
+  scalar_http_t(B, b, len, max, r, h, x);
 }
 
 }  // namespace rhp

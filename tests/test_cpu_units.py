@@ -50,7 +50,9 @@ def test_parse_batch_argument_errors_without_gpu():
     assert lib.rhp_parse_batch(ctypes.byref(b), None) == 0        # n == 0: nothing to do
     b.n = 5
     assert lib.rhp_parse_batch(ctypes.byref(b), None) == -22      # null pointers rejected
-    b.n, b.bytes, b.offsets, b.reqs, b.work, b.hdrs = 5, 1, 1, 1, 1, 1
+    b.n, b.bytes, b.offsets, b.reqs, b.work, b.hdrs = 5, 17, 8, 8, 8, 8
+    assert lib.rhp_parse_batch(ctypes.byref(b), None) == -22      # bytes not 16-byte aligned
+    b.bytes = 16
     b.max_headers = rhp.RHP_MAX_HEADERS + 1
     assert lib.rhp_parse_batch(ctypes.byref(b), None) == -22      # capacity limit
     b.max_headers, b.mode = 16, 7

@@ -13,6 +13,7 @@
 
 // PAT 0: random per lane (row r random, byte random)   PAT 1: same row, random byte
 // PAT 2: all lanes one address (broadcast)             PAT 3: lane-linear (a = lane*W)
+// PAT 5: ds_bpermute_b32 from a random lane (a table held one entry per lane)
 template <int W, int PAT>
 __global__ void k(uint32_t *out, int iters, uint32_t seed)
 {
@@ -37,6 +38,7 @@ __global__ void k(uint32_t *out, int iters, uint32_t seed)
     }
 #pragma unroll
     for (int j = 0; j < 8; j++) {
+      if (PAT == 5) { acc += (uint32_t) __builtin_amdgcn_ds_bpermute((int) (a[j] & 252u), (int) (acc ^ lane)); continue; }
       if (W == 1) acc += LDSP(uint8_t, a[j]);
       else if (W == 2) acc += LDSP(uint16_t, a[j]);
       else if (W == 4) acc += LDSP(uint32_t, a[j]);
@@ -87,6 +89,7 @@ int main()
   run<8, 0>(d_out, cus, "random row, random byte");
   run<8, 3>(d_out, cus, "lane-linear");
   run<1, 4>(d_out, cus, "one row, ascii byte");
+  run<4, 5>(d_out, cus, "ds_bpermute random lane");
   run<4, 4>(d_out, cus, "one row, ascii byte");
   return 0;
 }

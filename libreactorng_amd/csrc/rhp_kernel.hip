@@ -122,6 +122,7 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 #ifdef RHP_STAMPS
 /* diagnostic build only: per-wave cycle sums per loop section (never read by the kernel) */
 __device__ unsigned long long g_stamps[8192 * 8];
+__device__ unsigned long long g_stamps_end[8192];   /* entry -> end of the replay, per wave */
 #define RHP_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory"); \
     __builtin_amdgcn_sched_barrier(0); } while (0)
@@ -182,14 +183,94 @@ __device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64
   p.reqs[i] = r;
 }
 
+/* 28 bytes at b (any alignment) as 7 dwords, from three aligned 16-byte loads:
+ * the replay's scattered per-lane reads then cost 3 load instructions instead
+ * of one per byte (the batch buffer is 16-aligned and padded) */
+__device__ __forceinline__ void load28(const uint8_t *b, uint32_t (&d)[7])
+{
+  typedef __attribute__((address_space(1))) const u32x4_t gq;
+  const uintptr_t a = (uintptr_t) b, l = a & ~(uintptr_t) 15;
+  const u32x4_t q0 = *reinterpret_cast<gq *>(l), q1 = *reinterpret_cast<gq *>(l + 16), q2 = *reinterpret_cast<gq *>(l + 32);
+  const uint32_t c[12] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], q2[0], q2[1], q2[2], q2[3]};
+  const uint32_t k = (uint32_t) (a >> 2) & 3u, sh = (uint32_t) a & 3u;
+  uint32_t w[8];
+#pragma unroll
+  for (int m = 0; m < 8; m++) w[m] = k == 0 ? c[m] : k == 1 ? c[m + 1] : k == 2 ? c[m + 2] : c[m + 3];
+#pragma unroll
+  for (int m = 0; m < 7; m++) d[m] = __builtin_amdgcn_alignbyte(w[m + 1], w[m], sh);
+}
+
+/* byte j of a dword array (j constant after unrolling) */
+#define RHP_BYTE(d, j) (((d)[(j) >> 2] >> (8 * ((j) & 3))) & 0xffu)
+
+/* Case-insensitive compare of a parsed header name with a lower-case literal
+ * of n <= 28 bytes: OR 0x20 folds letters; the one non-letter, '-', could only
+ * collide with CR, which a parsed name cannot hold (tchar only) */
+template <uint32_t N>
+__device__ __forceinline__ bool name_is(const uint8_t *b, const rhp_hdr_t &h, const char (&lit)[N])
+{
+  constexpr uint32_t n = N - 1;
+  if (h.name_off == RHP_NAME_NULL || h.name_len != n) return false;
+  uint32_t d[7];
+  load28(b + h.name_off, d);
+  uint32_t diff = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < n; j++) diff |= (RHP_BYTE(d, j) | 0x20u) ^ (uint32_t) lit[j];
+  return diff == 0;
+}
+
+/* strtoull10 (rhp_scalar.h) over a 28-byte register window; the byte walk
+ * continues past it only for longer inputs */
+__device__ __forceinline__ uint64_t strtoull10_gpu(const uint8_t *s)
+{
+  uint32_t d[7];
+  load28(s, d);
+  uint32_t st = 0;
+  bool neg = false, ovf = false;
+  uint64_t v = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 28; j++) num_step(RHP_BYTE(d, j), st, neg, ovf, v);
+  for (const uint8_t *q = s + 28; st != 2; q++) num_step(*q, st, neg, ovf, v);
+  return ovf ? ~0ull : neg ? 0 - v : v;
+}
+
+/* http_frame (rhp_scalar.h) for the replay's common case, from the decode's
+ * hints (cand, crec: see the decode state) -- GET, no candidate header, or one
+ * that is Content-Length or neither; anything else takes http_frame.  Reads no
+ * header record and no method byte: on batches larger than the caches those
+ * re-reads are HBM traffic. */
+__device__ __forceinline__ bool http_frame_fast(const uint8_t *b, uint64_t len, const rhp_req_t &r, rhp_http_t *x,
+                                                uint32_t cand, uint32_t crec_lo, uint32_t crec_hi)
+{
+  const int64_t n = r.ret;
+  rhp_http_t o = {1, 0, (uint64_t) n, 0};
+  const uint32_t hdr = cand & 0x3fffffffu;
+  if (!(cand & 0x40000000u) && hdr != 0) {   /* not GET (http.c:198-202), some candidate */
+    if ((cand >> 31) || (hdr & (hdr - 1)) != 0) return false;
+    rhp_hdr_t hc;
+    hc.name_off = (uint16_t) crec_lo; hc.name_len = (uint16_t) (crec_lo >> 16);
+    hc.value_off = (uint16_t) crec_hi; hc.value_len = (uint16_t) (crec_hi >> 16);
+    if (name_is(b, hc, "transfer-encoding")) return false;   /* chunked framing: the general path */
+    if (name_is(b, hc, "content-length") && hc.value_len != 0) {
+      const uint64_t size = strtoull10_gpu(b + hc.value_off);
+      if (len < (uint64_t) n + size) {
+        o.result = 0; o.consumed = 0;
+      } else {
+        o.body_kind = 1; o.body_len = size; o.consumed = (uint64_t) n + size;
+      }
+    }
+  }
+  *x = o;
+  return true;
+}
+
 /* http_read_request framing of a request the DFA parsed (http mode only) */
 __device__ __forceinline__ void finish_http(const Params &p, uint32_t i, uint64_t off, uint64_t len, rhp_req_t r,
-                                            uint32_t cand)
+                                            uint32_t cand, uint32_t crec_lo, uint32_t crec_hi)
 {
-  /* cand: the framing candidates the decode left in http[i].consumed (bit 31:
-   * more than 31 headers, check all) */
-  http_frame(p.bytes_rw + off, len, r, p.hdrs + (uint64_t) i * p.max_headers, &p.http[i],
-             (cand >> 31) ? ~0ull : (uint64_t) cand);
+  const rhp_hdr_t *h = p.hdrs + (uint64_t) i * p.max_headers;
+  if (http_frame_fast(p.bytes_rw + off, len, r, &p.http[i], cand, crec_lo, crec_hi)) return;
+  http_frame(p.bytes_rw + off, len, r, h, &p.http[i], (cand >> 31) ? ~0ull : (uint64_t) (cand & 0x3fffffffu));
 }
 
 /* Params pointers are generic in the kernel's view (they sit in a struct);
@@ -330,7 +411,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    *   cur_lo: name part of the line in progress; rec_lo/rec_hi: the odd
    *   header record waiting for its pair (16-byte stores) */
   uint32_t kn = 0, A = 0, B = 0, ovf = 0, rl = 0, cur_lo = 0;
-  uint32_t cand = 0;                   /* http mode: headers whose name length is 14 or 17 (bit 31: index > 30) */
+  /* http mode, framing hints for the replay: cand bits 0..29 = headers whose
+   * name length is 14 or 17 (bit 31: such a header at index >= 30), bit 30 =
+   * the method is GET; crec = the first such header's record */
+  uint32_t cand = 0, crec_lo = 0, crec_hi = 0;
   uint32_t rec_lo = 0, rec_hi = 0;
   bool pend_ok = false;                /* pend: the lane's next request */
   uint32_t pend = 0;
@@ -420,7 +504,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const bool odd = (kn & 256u) != 0;
     if (p.mode == RHP_MODE_HTTP) {   /* uniform: framing candidates only in http mode */
       const uint32_t nlen = r_lo >> 16, hidx = (kn >> 8) - 1u;
-      cand |= done && (nlen == 14u || nlen == 17u) ? (hidx < 31u ? 1u << hidx : 0x80000000u) : 0u;
+      const bool cnd = done && (nlen == 14u || nlen == 17u);
+      const bool first = cnd && (cand & 0xbfffffffu) == 0;
+      crec_lo = first ? r_lo : crec_lo;
+      crec_hi = first ? r_hi : crec_hi;
+      cand |= cnd ? (hidx < 30u ? 1u << hidx : 0x80000000u) : 0u;
     }
     rec_lo = done && odd ? r_lo : rec_lo;
     rec_hi = done && odd ? r_hi : rec_hi;
@@ -493,7 +581,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       r.flags = p.mode == RHP_MODE_HTTP ? (uint16_t) kDeferFrame : (uint16_t) 0;   /* framing: replay */
       if (p.mode == RHP_MODE_HTTP) {
         *wg_deferred = 1u;
-        *GLOBAL(uint64_t, &p.http[cur].consumed) = cand;   /* framing candidates for the replay */
+        /* framing hints for the replay, in the record it will overwrite */
+        typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+        *GLOBAL(u32x4a4, &p.http[cur]) = u32x4a4{cand, 0u, crec_lo, crec_hi};
       }
     } else if (bad) {
       r.ret = -1;
@@ -634,7 +724,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (cur_len > kFastMaxLen) s0 = S_SLOW;
       st = start_index(s0);
       pos = -(int32_t) mis;
-      kn = A = B = ovf = rl = cand = 0;
+      kn = A = B = ovf = rl = 0;
+      /* GET: the request's first four bytes are "GET " (the DFA path parses
+       * the method from byte 0), read from the window already in registers */
+      const uint32_t head = __builtin_amdgcn_alignbyte(W[0][1], W[0][0], mis);
+      cand = head == ('G' | 'E' << 8 | 'T' << 16 | (uint32_t) ' ' << 24) ? 0x40000000u : 0u;
     }
     if (nw_kind) cur_ptr = nw & ~3u;
     const bool pend_ready = pend_ok;   /* assigned before this block: p_o0/p_o1 valid */
@@ -712,17 +806,30 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const u32x4 rv = *GLOBAL(const u32x4, p.reqs + i);
       __builtin_memcpy(&r, &rv, sizeof r);
       const uint64_t off = p.offsets[i], end = p.offsets[i + 1];
-      const uint32_t cand = p.mode == RHP_MODE_HTTP ? (uint32_t) p.http[i].consumed : 0u;
+      typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+      const u32x4a4 hint = p.mode == RHP_MODE_HTTP ? *GLOBAL(const u32x4a4, &p.http[i]) : u32x4a4{0u, 0u, 0u, 0u};
       const uint32_t f = r.flags;
       if (!(f & (kDeferExact | kDeferFrame))) continue;
       if (f & kDeferExact) {
+#ifndef RHP_EXP_NOEXACT   /* timing experiment: exact-path requests left unfinished */
         finish_exact(p, i, off, end - off);
+#endif
       } else {
+#ifdef RHP_EXP_NOFRAME    /* timing experiment: framing left undone */
+        continue;
+#endif
         r.flags = 0;
-        finish_http(p, i, off, end - off, r, cand);
+        finish_http(p, i, off, end - off, r, hint[0], hint[2], hint[3]);
         p.reqs[i].flags = 0;
       }
     }
+  }
+#endif
+#ifdef RHP_STAMPS
+  if (lane == 0) {
+    unsigned long long t_end = 0;
+    RHP_STAMP(t_end);
+    g_stamps_end[(blockIdx.x * WAVES + wave) % 8192] = t_end - t_entry;
   }
 #endif
 }
@@ -788,6 +895,11 @@ const char *rhp_version(void) { return "rhp 0.4.0 (gfx950)"; }
 int rhp_debug_stamps(unsigned long long *host)
 {
   return (int) hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(g_stamps), 0, hipMemcpyDeviceToHost);
+}
+/* ... and the per-wave entry -> end-of-replay spans (8192 u64) */
+int rhp_debug_stamps_end(unsigned long long *host)
+{
+  return (int) hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps_end), sizeof(g_stamps_end), 0, hipMemcpyDeviceToHost);
 }
 #endif
 

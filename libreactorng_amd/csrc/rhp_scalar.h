@@ -181,7 +181,8 @@ RHP_HD void num_step(uint32_t c, uint32_t &st, bool &neg, bool &ovf, uint64_t &v
   }
   if (st != 1 || !digit) return;
   const uint64_t d = c - '0';
-  ovf |= v > (~0ull - d) / 10;
+  /* v * 10 + d > 2^64 - 1  <=>  v > 1844674407370955161, or v equal to it and d > 5 */
+  ovf |= v > 1844674407370955161ull || (v == 1844674407370955161ull && d > 5u);
   v = v * 10 + d;
 }
 

@@ -51,6 +51,15 @@ if ng:
     print("  mean per XCD (g % 8): " + " ".join(f"{v:.0f}" for v in xcd))
     slow = np.argsort(wg)[-8:]
     print("  slowest workgroups: " + " ".join(str(int(g)) for g in slow))
+if ng and hasattr(lib, "rhp_debug_stamps_end"):
+    se = np.zeros(8192, dtype=np.uint64)
+    lib.rhp_debug_stamps_end.argtypes = [ctypes.c_void_p]
+    assert lib.rhp_debug_stamps_end(se.ctypes.data) == 0
+    end = se.astype(np.float64)[used]
+    wg_loop = whole[: ng * W].reshape(ng, W).max(axis=1)
+    wg_end = end[: ng * W].reshape(ng, W).max(axis=1)
+    print(f"  per-workgroup loop end (last wave) mean {wg_loop.mean():.0f}, replay end mean {wg_end.mean():.0f} max {wg_end.max():.0f}"
+          f"  -> replay {100 * (wg_end - wg_loop).mean() / wg_end.mean():.1f} % of the workgroup span")
 if ng:
     per_idx = whole[: ng * W].reshape(ng, W)
     print("  mean entry->exit by wave index in workgroup: " + " ".join(f"{v / 1000:.0f}k" for v in per_idx.mean(axis=0)))

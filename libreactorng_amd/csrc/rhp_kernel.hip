@@ -6,24 +6,27 @@
  * HBM.  Design:
  *
  *  - one request per lane, 64 requests per wave in flight; every lane runs the
- *    byte DFA of rhp_dfa.h in lockstep.  One step is one LDS read and two VALU:
- *        a     = v_perm(state, window dword, sel)   = state * 256 + byte
- *        state = T8[a]                               ds_read_u8, next index
- *        ev    = v_alignbit(state, ev, 1)            odd index = event bit
- *    no LDS write and no divergence on the byte path;
- *  - a step waits on its own LDS read (a dependent chain per lane), so the
- *    throughput comes from waves in flight: the lane state is kept small
- *    (<= 64 VGPRs: 8 waves per SIMD) and the window staging single-buffered
- *    (4 KiB per wave: two 16-wave workgroups per CU);
- *  - lanes stream their request in 64-byte windows: the wave fetches its 64
- *    lanes' next windows with four LDS-DMA loads (16 windows x 64 B each), a
- *    whole block ahead of use; every lane also holds its NEXT request's
- *    offsets, so a request switch never waits on a dependent load;
- *  - once per block the event mask is decoded (rhp_dfa.h dec_event) into the
- *    request-line record and header records (stored in 16-byte pairs);
+ *    pair DFA of rhp_dfa.h in lockstep, two bytes per table read:
+ *        k0, k1 = class[b0], class[b1]               two ds_read_u8, a chunk ahead
+ *        a      = v_perm(idx, codes, sel)            = idx * 256 + k0 * 16 + k1
+ *        idx    = T2[a]                              one dependent ds_read_u8
+ *        ev     = v_alignbit(idx, ev, 2)             low index bits = event bits
+ *    no LDS write and no divergence on the byte path; the kernel is bound by
+ *    LDS issue;
+ *  - lanes stream their request in 128-byte windows = whole HBM lines: the
+ *    wave fetches its 64 lanes' next windows with eight LDS-DMA loads (8
+ *    lines each) a whole block ahead of use, into a single-buffered staging
+ *    area (8 KiB per wave, one 16-wave workgroup per CU); every lane also
+ *    holds its NEXT request's offsets, so a request switch never waits on a
+ *    dependent load;
+ *  - once per block the event masks are decoded, straight-line per event
+ *    (or per CO+EOL pair), into the request-line and header records (stored
+ *    in 16-byte pairs); in http mode the decode also leaves framing hints
+ *    (GET, the Content-Length / Transfer-Encoding candidates);
  *  - a request the table cannot decide alone (S_SLOW, a terminal at/after
  *    len, no terminal by the end of its buffer) and http framing are finished
- *    after the loop by the exact scalar path (rhp_scalar.h).
+ *    after the loop by the workgroup's replay (rhp_scalar.h exact path through
+ *    a 16-byte line cache; framing from the hints).
  *
  * The algorithm is mirrored block for block by rhp_emu.cpp (CPU tests).
  */
@@ -85,7 +88,13 @@ enum : uint32_t {
   kStageWave = 64 * kBlock,                      /* one window per lane, single-buffered */
   kPark = 0,                                     /* the DONE index: idle lanes step here */
   kDeferExact = 0x8000u,                         /* reqs[i].flags while deferred (kernel-internal) */
-  kDeferFrame = 0x4000u
+  kDeferFrame = 0x4000u,
+  /* workgroup pool area after the staging buffers: counters, then the long-
+   * request bitmap (ranges up to kOrderSpan requests) and list */
+  kPoolWords = 8,                                /* counter, replay flag, list length, list cursor */
+  kOrderSpan = 8192,
+  kListCap = 1536,
+  kPoolBytes = 4 * kPoolWords + kOrderSpan / 8 + 2 * kListCap
 };
 static_assert(kBlock == 64 || kBlock == 128, "64- or 128-byte windows");
 static_assert(idx2(S_DONE, 0) == kPark && idx8(S_DONE) == kPark, "parked lanes sit in DONE");
@@ -368,7 +377,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const u32x4 *src = reinterpret_cast<const u32x4 *>(&g_table);
     u32x4 *dst = reinterpret_cast<u32x4 *>(lds);
     for (uint32_t k = tid; k < kTableBytes / 16; k += WAVES * 64) dst[k] = src[k];
-    if (tid < 2) reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave)[tid] = 0;   /* pool counter, replay flag */
+    /* pool counters and the long-request bitmap start at zero */
+    for (uint32_t k = tid; k < kPoolWords + kOrderSpan / 32; k += WAVES * 64)
+      reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave)[k] = 0;
   }
   __syncthreads();
 
@@ -385,6 +396,21 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   const uint32_t wg_lo = min(blockIdx.x * p.span, p.n), wg_hi = min(wg_lo + p.span, p.n);
   uint32_t *wg_counter = reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave);
   uint32_t *wg_deferred = wg_counter + 1;   /* some request of the range needs the replay */
+  /* Long requests first.  With lengths as uneven as config 3's, the requests
+   * drawn last decide when a wave finishes; the first iteration (which only
+   * waits for the first windows) lists the range's requests longer than twice
+   * its mean, and refills hand those out before the rest (simulated: -20 %
+   * wave-iterations on config 3).  Ranges above kOrderSpan keep plain order. */
+  uint32_t *list_n = wg_counter + 2, *list_next = wg_counter + 3;
+  uint32_t *long_bits = wg_counter + kPoolWords;
+  uint16_t *long_list = reinterpret_cast<uint16_t *>(long_bits + kOrderSpan / 32);
+#ifdef RHP_NO_ORDER   /* experiment: plain range order */
+  const bool order_on = false;
+#else
+  const bool order_on = wg_hi - wg_lo <= kOrderSpan;
+#endif
+  bool list_dry = !order_on;
+  bool first_iter = true;   /* the list is complete only after the scan (before the loop) */
   bool pool_dry = wg_lo >= wg_hi;
   const uint64_t base = pool_dry ? 0 : (p.offsets[wg_lo] & ~(uint64_t) 3);
   const uint8_t *wbytes = p.bytes + base;
@@ -429,23 +455,62 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 
   /* give every lane without a pending request one from the pool; the offsets
    * loads are only consumed at the top of the next block */
+  auto take = [&](uint32_t i) {
+    pend = i;
+    /* only the low dwords: a batch is below 4 GiB, so offsets relative to
+     * `base` and lengths are exact modulo 2^32 */
+    const uint32_t *o = reinterpret_cast<const uint32_t *>(p.offsets + pend);
+    pend_o0 = *GLOBAL(const uint32_t, o);
+    pend_o1 = *GLOBAL(const uint32_t, o + 2);
+    pend_ok = true;
+  };
   auto refill_pend = [&]() {
-    const uint64_t want = __ballot(!pend_ok);
-    if (!want || pool_dry) return;
-    const uint32_t cnt = (uint32_t) __popcll(want);
-    uint32_t b0 = 0;
-    if (lane == 0) b0 = atomicAdd(wg_counter, cnt);
-    b0 = wg_lo + __builtin_amdgcn_readfirstlane(b0);
-    if (b0 + cnt >= wg_hi) pool_dry = true;
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
-    if (!pend_ok && b0 + rank < wg_hi) {
-      pend = b0 + rank;
-      /* only the low dwords: a batch is below 4 GiB, so offsets relative to
-       * `base` and lengths are exact modulo 2^32 */
-      const uint32_t *o = reinterpret_cast<const uint32_t *>(p.offsets + pend);
-      pend_o0 = *GLOBAL(const uint32_t, o);
-      pend_o1 = *GLOBAL(const uint32_t, o + 2);
-      pend_ok = true;
+    uint64_t want = __ballot(!pend_ok);
+    if (!want || (pool_dry && list_dry)) return;
+    if (!list_dry && !first_iter) {   /* the long list first */
+      const uint32_t cnt = (uint32_t) __popcll(want);
+      uint32_t b0 = 0;
+      if (lane == 0) b0 = atomicAdd(list_next, cnt);
+      b0 = __builtin_amdgcn_readfirstlane(b0);
+      const uint32_t nl = min(*list_n, (uint32_t) kListCap);
+      if (b0 + cnt >= nl) list_dry = true;
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
+      if (!pend_ok && b0 + rank < nl) take(wg_lo + long_list[b0 + rank]);
+      want = __ballot(!pend_ok);
+    }
+    /* the range in order, skipping the listed requests (a few rounds at most) */
+    while (want && !pool_dry) {
+      const uint32_t cnt = (uint32_t) __popcll(want);
+      uint32_t b0 = 0;
+      if (lane == 0) b0 = atomicAdd(wg_counter, cnt);
+      b0 = wg_lo + __builtin_amdgcn_readfirstlane(b0);
+      if (b0 + cnt >= wg_hi) pool_dry = true;
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
+      const uint32_t i = b0 + rank, k = i - wg_lo;
+      if (!pend_ok && i < wg_hi && !(order_on && ((long_bits[k >> 5] >> (k & 31)) & 1u))) take(i);
+      want = __ballot(!pend_ok);
+    }
+  };
+
+  /* the long-request scan (see order_on), once, over the part of the range the
+   * first refill did not hand out */
+  auto scan_long = [&]() {
+    const uint32_t span_n = wg_hi - wg_lo, first_n = min(span_n, (uint32_t) (WAVES * 64));
+    if (span_n <= first_n) return;
+    /* long: length * count > 2 * the range's bytes (no division) */
+    const uint64_t twice = 2u * (p.offsets[wg_hi] - p.offsets[wg_lo]);
+    /* a wave scans its slice only if its own first requests (offsets already
+     * loaded) include a long one: uniform batches skip the scan */
+    if (!__ballot(pend_ok && (uint64_t) (pend_o1 - pend_o0) * span_n > twice)) return;
+    for (uint32_t k = first_n + tid; k < span_n; k += WAVES * 64) {
+      const uint64_t o0 = p.offsets[wg_lo + k], o1 = p.offsets[wg_lo + k + 1];
+      if ((o1 - o0) * span_n > twice) {
+        const uint32_t at = atomicAdd(list_n, 1u);
+        if (at < kListCap) {
+          long_list[at] = (uint16_t) k;
+          atomicOr(&long_bits[k >> 5], 1u << (k & 31));
+        }
+      }
     }
   };
 
@@ -683,6 +748,15 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   };
 
   refill_pend();
+  /* The first iteration, peeled: there is no block to decode or switch yet.
+   * Issue the first windows, then (while they land) the long-request scan; the
+   * barrier makes the list complete before any wave's next refill. */
+  wait_vm0();   /* the pending offsets */
+  nw = pend_ok ? ((pend_o0 & ~3u) - (uint32_t) base) | 2u : 0u;
+  issue();
+  if (order_on) scan_long();
+  __syncthreads();
+  first_iter = false;
 
 #ifdef RHP_STAMPS
   unsigned long long t0 = 0, t1 = 0, acc[6] = {0, 0, 0, 0, 0, 0}, t_loop = 0;
@@ -852,7 +926,7 @@ int g_cus = 0;
 template <int WAVES>
 int launch_dfa(const Params &prm, hipStream_t s)
 {
-  const size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + 16;
+  const size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES>),

@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <hip/hip_runtime_api.h>
 
 #include "reactor.h"
@@ -34,7 +35,26 @@ static __thread struct
   rhp_http_t  *h_http;
   void        *d_bytes, *d_off, *d_req, *d_hdr, *d_http, *d_work;
   hipStream_t  stream;
+  /* RHP_REACTOR_STATS=1: rounds, requests and time spent in the parser, printed at exit */
+  int          stats;
+  int          diag_host;   /* RHP_REACTOR_DIAG=hostparse: gpu-mode buffers, host parse (diagnostic) */
+  uint64_t     st_rounds, st_requests, st_ns;
 } B;
+
+static uint64_t now_ns(void)
+{
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t) ts.tv_sec * 1000000000u + (uint64_t) ts.tv_nsec;
+}
+
+static void print_stats(void)
+{
+  fprintf(stderr, "reactor parser %s: %llu rounds, %llu requests (%.1f per round), %.1f us per round\n",
+          B.parser == PARSER_GPU ? "gpu" : "host", (unsigned long long) B.st_rounds, (unsigned long long) B.st_requests,
+          B.st_rounds ? (double) B.st_requests / (double) B.st_rounds : 0.0,
+          B.st_rounds ? (double) B.st_ns / 1e3 / (double) B.st_rounds : 0.0);
+}
 
 static void die(const char *what, int e)
 {
@@ -51,6 +71,11 @@ static int parser(void)
   {
     const char *e = getenv("RHP_REACTOR_PARSER");
     B.parser = e && strcmp(e, "host") == 0 ? PARSER_HOST : PARSER_GPU;
+    const char *st = getenv("RHP_REACTOR_STATS");
+    if ((B.stats = st && *st == '1'))
+      atexit(print_stats);
+    const char *dg = getenv("RHP_REACTOR_DIAG");
+    B.diag_host = dg && strcmp(dg, "hostparse") == 0;
     if (B.parser == PARSER_GPU)
     {
       int n = 0;
@@ -98,10 +123,13 @@ static void dev_free(void **p)
 uint8_t *reactor_batch_reserve(size_t bytes, uint32_t n)
 {
   (void) parser();
+  const uint64_t t0 = B.stats ? now_ns() : 0;
   const size_t need = bytes + RHP_PAD;
   if (need > B.cap_bytes)
   {
-    size_t c = B.cap_bytes ? B.cap_bytes : 1u << 16;
+    /* generous first capacities: growing pinned and device buffers costs
+     * milliseconds per step (page pinning, frees that synchronise) */
+    size_t c = B.cap_bytes ? B.cap_bytes : 1u << 20;
     while (c < need)
       c *= 2;
     host_free(B.h_bytes);
@@ -115,7 +143,7 @@ uint8_t *reactor_batch_reserve(size_t bytes, uint32_t n)
   }
   if (n + 1 > B.cap_n)
   {
-    size_t c = B.cap_n ? B.cap_n : 256;
+    size_t c = B.cap_n ? B.cap_n : 4096;
     while (c < n + 1u)
       c *= 2;
     host_free(B.h_off);
@@ -144,6 +172,8 @@ uint8_t *reactor_batch_reserve(size_t bytes, uint32_t n)
     }
     B.cap_n = c;
   }
+  if (B.stats)
+    B.st_ns += now_ns() - t0;
   return B.h_bytes;
 }
 
@@ -154,9 +184,10 @@ uint64_t *reactor_batch_offsets(void)
 
 int reactor_batch_run(uint32_t n, size_t bytes, reactor_batch_result_t *out)
 {
+  const uint64_t t0 = B.stats ? now_ns() : 0;
   memset(B.h_bytes + bytes, 0, RHP_PAD);
   B.h_off[n] = bytes;
-  if (B.parser == PARSER_HOST)
+  if (B.parser == PARSER_HOST || B.diag_host)
   {
     rhp_batch_t b = {
       .bytes = B.h_bytes, .bytes_rw = B.h_bytes, .offsets = B.h_off, .bytes_size = bytes + RHP_PAD, .n = n,
@@ -188,6 +219,12 @@ int reactor_batch_run(uint32_t n, size_t bytes, reactor_batch_result_t *out)
         HIP(hipMemcpy(B.h_bytes + B.h_off[i], (uint8_t *) B.d_bytes + B.h_off[i], x->consumed,
                       hipMemcpyDeviceToHost));
     }
+  }
+  if (B.stats)
+  {
+    B.st_rounds++;
+    B.st_requests += n;
+    B.st_ns += now_ns() - t0;
   }
   out->bytes = B.h_bytes;
   out->reqs = B.h_req;

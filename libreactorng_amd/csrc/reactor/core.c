@@ -284,8 +284,38 @@ void reactor_poll_remove(reactor_t id)
   core.dead[core.dead_n++] = p;
 }
 
+/* RHP_REACTOR_STATS=1: epoll_wait calls and the time blocked in them, at exit */
+static int core_stats = -1;
+static uint64_t core_wait_ns, core_waits, core_next_ns, core_events_ns, core_events, core_events_cpu_ns;
+static uint64_t core_cpu_ns(void)
+{
+  struct timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (uint64_t) ts.tv_sec * 1000000000u + (uint64_t) ts.tv_nsec;
+}
+static uint64_t core_ns(void)
+{
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t) ts.tv_sec * 1000000000u + (uint64_t) ts.tv_nsec;
+}
+static void core_print_stats(void)
+{
+  fprintf(stderr, "reactor loop: %llu epoll_wait calls, %.1f ms blocked; deferred calls %.1f ms; %llu events handled in %.1f ms"
+          " (thread CPU %.1f ms)\n", (unsigned long long) core_waits, (double) core_wait_ns / 1e6, (double) core_next_ns / 1e6,
+          (unsigned long long) core_events, (double) core_events_ns / 1e6, (double) core_events_cpu_ns / 1e6);
+}
+
 void reactor_loop_once(void)
 {
+  if (core_stats < 0)
+  {
+    const char *st = getenv("RHP_REACTOR_STATS");
+    core_stats = st && *st == '1';
+    if (core_stats)
+      atexit(core_print_stats);
+  }
+  const uint64_t n0 = core_stats > 0 ? core_ns() : 0;
   if (core.next_n)
   {
     reactor_user_t **run = core.next;
@@ -301,16 +331,33 @@ void reactor_loop_once(void)
     }
     free(run);
   }
+  if (core_stats > 0)
+    core_next_ns += core_ns() - n0;
   if (core.users > core.next_n)
   {
     struct epoll_event ev[256];
+    struct timespec w0, w1;
+    if (core_stats) clock_gettime(CLOCK_MONOTONIC, &w0);
     int n = epoll_wait(core.epfd, ev, 256, core.next_n ? 0 : -1);
+    if (core_stats)
+    {
+      clock_gettime(CLOCK_MONOTONIC, &w1);
+      core_wait_ns += (uint64_t) (w1.tv_sec - w0.tv_sec) * 1000000000u + (uint64_t) w1.tv_nsec - (uint64_t) w0.tv_nsec;
+      core_waits++;
+    }
     core.time = 0;
+    const uint64_t e0 = core_stats > 0 ? core_ns() : 0, c0 = core_stats > 0 ? core_cpu_ns() : 0;
     for (int i = 0; i < n; i++)
     {
       poll_user_t *p = ev[i].data.ptr;
       if (!p->dead)
         reactor_call(&p->user, REACTOR_CALL, ev[i].events);
+    }
+    if (core_stats > 0)
+    {
+      core_events_ns += core_ns() - e0;
+      core_events_cpu_ns += core_cpu_ns() - c0;
+      core_events += n > 0 ? (uint64_t) n : 0;
     }
     reactor_reap();
   }

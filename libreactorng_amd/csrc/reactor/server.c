@@ -258,8 +258,30 @@ static bool server_session_dispatch(server_session_t *s, const piece_t *pc, size
   return !more;
 }
 
+/* RHP_REACTOR_STATS=1: time per round phase (split+pack, parse, dispatch), at exit */
+static int round_stats = -1;
+static uint64_t rs_pack_ns, rs_parse_ns, rs_dispatch_ns, rs_rounds;
+static uint64_t rs_now(void)
+{
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t) ts.tv_sec * 1000000000u + (uint64_t) ts.tv_nsec;
+}
+static void rs_print(void)
+{
+  fprintf(stderr, "server rounds: %llu, split+pack %.1f ms, parse %.1f ms, dispatch %.1f ms\n", (unsigned long long) rs_rounds,
+          (double) rs_pack_ns / 1e6, (double) rs_parse_ns / 1e6, (double) rs_dispatch_ns / 1e6);
+}
+
 static void server_batch_round(server_t *server, round_t *r)
 {
+  if (round_stats < 0)
+  {
+    const char *st = getenv("RHP_REACTOR_STATS");
+    if ((round_stats = st && *st == '1'))
+      atexit(rs_print);
+  }
+  const uint64_t t0 = round_stats ? rs_now() : 0;
   r->n_sessions = r->n_pieces = 0;
   size_t bytes = 0;
   while (!list_is_empty(&server->queue))
@@ -307,8 +329,10 @@ static void server_batch_round(server_t *server, round_t *r)
     }
   }
   reactor_batch_result_t res = {0};
+  const uint64_t t1 = round_stats ? rs_now() : 0;
   if (r->n_pieces)
     (void) reactor_batch_run((uint32_t) r->n_pieces, bytes, &res);
+  const uint64_t t2 = round_stats ? rs_now() : 0;
 
   size_t k = 0;
   for (size_t i = 0; i < r->n_sessions; i++)
@@ -328,6 +352,14 @@ static void server_batch_round(server_t *server, round_t *r)
     r->sessions[i]->in_round = false;
     if (r->sessions[i]->dead)
       free(r->sessions[i]);
+  }
+  if (round_stats)
+  {
+    const uint64_t t3 = rs_now();
+    rs_pack_ns += t1 - t0;
+    rs_parse_ns += t2 - t1;
+    rs_dispatch_ns += t3 - t2;
+    rs_rounds++;
   }
 }
 

@@ -250,6 +250,27 @@ constexpr bool classes_exact()
 }
 static_assert(classes_exact(), "byte classes must not split any transition");
 
+/*
+ * Run skipping.  In the path token (ADVANCE_TOKEN, picohttpparser.c:71-94) and
+ * inside a header value (get_token_to_eol, :134-195) every byte that is not
+ * SP, a CTL or DEL keeps the state and fires no event -- the cases the
+ * reference's findchar_fast pre-scan skips 16 bytes at a time (:105-132).  A
+ * chunk made only of such bytes therefore leaves a lane in S_PATH, or moves
+ * it from S_VALUE / S_VWS to S_VALUE, with an all-zero event mask; the kernel
+ * skips the table walk for a chunk when that holds for every busy lane of the
+ * wave (wave-uniform: an LDS read costs the same with idle lanes masked off).
+ */
+constexpr bool c_run(uint32_t c) { return c > 0x20u && c != 0x7fu; }
+constexpr bool runs_exact()
+{
+  for (uint32_t c = 0; c < 256; c++) {
+    if (!c_run(c)) continue;
+    if (step(S_PATH, c) != S_PATH || step(S_VALUE, c) != S_VALUE || step(S_VWS, c) != S_VALUE) return false;
+  }
+  return true;
+}
+static_assert(runs_exact(), "run bytes keep S_PATH / move S_VALUE, S_VWS to S_VALUE without an event");
+
 RHP_DHD constexpr uint32_t idx2(uint32_t s, uint32_t e)
 {
   return s < S_NUM_PLAIN ? 4u * s + e : 4u * (s - S_NUM_PLAIN) + e;

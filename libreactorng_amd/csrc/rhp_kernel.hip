@@ -46,6 +46,24 @@ using namespace rhp;
 #ifndef RHP_PAIR
 #define RHP_PAIR 1   /* 1: pair DFA (rhp_dfa.h Table2), 0: byte DFA (Table8) */
 #endif
+#define RHP_NT_ALIGNED (-1)
+#ifndef RHP_LDS_AUX
+#define RHP_LDS_AUX RHP_NT_ALIGNED   /* window load cache policy: 0 normal, 2 nt, -1 nt when line-aligned (issue) */
+#endif
+#ifndef RHP_ST_NT
+#define RHP_ST_NT 0     /* 1: record stores non-temporal */
+#endif
+#if RHP_ST_NT
+#define RHP_ST_POLICY " nt"
+#else
+#define RHP_ST_POLICY ""
+#endif
+#ifndef RHP_EARLY
+#define RHP_EARLY 0     /* issue the next window before the decode (128-B windows); measured no gain, profiles/r01/v9 */
+#endif
+#ifndef RHP_SKIP
+#define RHP_SKIP 0   /* pair DFA: skip chunks of run bytes wave-uniformly (rhp_dfa.h runs_exact); measured no gain, profiles/r01/v9 */
+#endif
 #if RHP_PAIR
 __device__ const Table2 g_table = make_table2();
 #define kTableBytes kTable2Bytes
@@ -97,6 +115,7 @@ enum : uint32_t {
   kPoolBytes = 4 * kPoolWords + kOrderSpan / 8 + 2 * kListCap
 };
 static_assert(kBlock == 64 || kBlock == 128, "64- or 128-byte windows");
+static_assert(!RHP_EARLY || kBlock == 128, "early issue needs whole-line windows");
 static_assert(idx2(S_DONE, 0) == kPark && idx8(S_DONE) == kPark, "parked lanes sit in DONE");
 
 /* LDS byte address of part q (16 B) of lane w's window inside the staging
@@ -327,7 +346,7 @@ __device__ __forceinline__ void store_pair_lanes(uint64_t mask, rhp_hdr_t *dst, 
   uint64_t saved;
   asm volatile("s_mov_b64 %0, exec\n\t"
                "s_mov_b64 exec, %1\n\t"
-               "global_store_dwordx4 %2, %3, off\n\t"
+               "global_store_dwordx4 %2, %3, off" RHP_ST_POLICY "\n\t"
                "s_mov_b64 exec, %0\n\t"
                "s_nop 1"
                : "=&s"(saved)
@@ -337,13 +356,21 @@ __device__ __forceinline__ void store_pair_lanes(uint64_t mask, rhp_hdr_t *dst, 
 __device__ __forceinline__ void store_one(rhp_hdr_t *dst, u32x2 v)
 {
   typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+#if RHP_ST_NT
+  __builtin_nontemporal_store(v, GLOBAL(u32x2a4, dst));
+#else
   *GLOBAL(u32x2a4, dst) = v;
+#endif
 }
 __device__ __forceinline__ void store_req(rhp_req_t *dst, const rhp_req_t &r)
 {
   u32x4 v;
   __builtin_memcpy(&v, &r, sizeof r);
+#if RHP_ST_NT
+  __builtin_nontemporal_store(v, GLOBAL(u32x4, dst));
+#else
   *GLOBAL(u32x4, dst) = v;
+#endif
 }
 __device__ __forceinline__ void store_http_bad(rhp_http_t *dst)
 {
@@ -707,6 +734,49 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       }
     }
   };
+#elif RHP_SKIP
+  /* 16 bytes are all run bytes (rhp_dfa.h c_run: > 0x20 and not DEL).  SWAR,
+   * exact as an existence test: (x - 0x21..) & ~x has a byte's top bit set for
+   * the lowest byte below 0x21 (bytes >= 0x80 are masked by ~x and borrow
+   * nothing), and likewise for the zero bytes of x ^ 0x7f.. (DEL) */
+  auto run16 = [&](const u32x4 &c) -> bool {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      const uint32_t x = c[d], y = x ^ 0x7f7f7f7fu;
+      acc |= ((x - 0x21212121u) & ~x) | ((y - 0x01010101u) & ~y);
+    }
+    return (acc & 0x80808080u) == 0;
+  };
+  /* Chunks whose bytes keep every busy lane of the wave in a run state
+   * (S_PATH, S_VALUE, S_VWS) are skipped (rhp_dfa.h runs_exact): the state
+   * becomes the run's plain index and the chunk's 16 event bits are zero.
+   * The class reads of chunk q+1 are issued ahead (during chunk q's chain)
+   * unless chunk q was skipped: inside a run the next chunk is likely skipped
+   * too, and its reads would be wasted. */
+  auto steps_chunks = [&](const u32x4 *Wc, int nchunks, uint32_t *evw) {
+    uint32_t k[16], pc[4];
+    bool ahead = false;   /* k holds the classes of chunk q */
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      if (q >= nchunks) break;
+      const uint32_t s = st & ~1u;   /* plain row (e = 0 or 1) */
+      const bool in_run = s == 4u * S_PATH || s == 4u * S_VALUE || s == 4u * S_VWS;
+      if (!__builtin_amdgcn_ballot_w64(!in_run) && !__builtin_amdgcn_ballot_w64(!run16(Wc[q]))) {
+        st = s == 4u * S_PATH ? 4u * S_PATH : 4u * S_VALUE;
+        evw[q >> 1] >>= 16;
+        ahead = false;
+        continue;
+      }
+      if (!ahead) classes16(Wc[q], k);
+      codes(k, pc);
+      if (q + 1 < nchunks) classes16(Wc[q + 1], k);
+      ahead = q + 1 < nchunks;
+      __builtin_amdgcn_sched_barrier(0);
+      steps16(pc, evw[q >> 1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
 #else
   auto steps_chunks = [&](const u32x4 *Wc, int nchunks, uint32_t *evw) {
     uint32_t k[16], pc[4];
@@ -739,11 +809,24 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       a[i] &= 255u;
 #endif
     }
+#if RHP_LDS_AUX == RHP_NT_ALIGNED
+    /* Cache policy per wave and window: when every window is one whole HBM
+     * line (line-aligned requests), no line is read by two windows and the
+     * loads go non-temporal (config 2 +19 %, config 5 +9 %); windows that
+     * straddle lines share their edge lines with the neighbouring requests'
+     * windows, which then hit in L2 (non-temporal: config 3 -5 %) */
+    const bool aligned = !(nw & 3u) || ((uint32_t) (uintptr_t) (wbytes + src) & (kBlock - 1u)) == 0;
+    const bool nt = !__builtin_amdgcn_ballot_w64(!aligned);
+#else
+    constexpr bool nt = RHP_LDS_AUX == 2;
+#endif
 #pragma unroll
     for (int i = 0; i < (int) kParts; i++) {
       const uint32_t part = dma_part(dma_window((uint32_t) i, lane), lane);
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(wbytes + a[i] + 16u * part),
-                                       (__attribute__((address_space(3))) void *) (lds + stage + 1024u * i), 16, 0, 0);
+      const void *g = reinterpret_cast<const void *>(wbytes + a[i] + 16u * part);
+      __attribute__((address_space(3))) void *l = (__attribute__((address_space(3))) void *) (lds + stage + 1024u * i);
+      if (nt) __builtin_amdgcn_global_load_lds(g, l, 16, 0, 2);
+      else __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
     }
   };
 
@@ -777,6 +860,31 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const uint32_t p_o0 = pend_o0, p_o1 = pend_o1;
 #pragma unroll
     for (int q = 0; q < kWRegs; q++) W[q] = *reinterpret_cast<const u32x4 *>(lds + stage + stage_off(lane, q));
+    const uint32_t nw_in = nw;   /* the window now in W */
+#if RHP_EARLY
+    /* [E] early: the next window is issued before the decode and the switch,
+     * so a wave has loads in flight through them as well as through its walk.
+     * The switch and finalize are predicted from what is known already: W is
+     * pend's first window (kind 2) -> pend's second window if it has one;
+     * otherwise cur continues unless its state is terminal (the decode's
+     * max_headers stop is the one outcome not foreseen: that lane loads one
+     * unused window) -> else the first window of a pend assigned earlier. */
+    {
+      const uint32_t k = nw_in & 3u;
+      uint32_t nn = 0;
+      if (k == 2) {
+        const uint32_t mis = p_o0 & 3u;
+        if (kBlock - mis < p_o1 - p_o0) nn = ((nw_in & ~3u) + kBlock) | 1u;
+      } else {
+        const bool live = k == 1 && has && !t_done(st) && !t_err(st) && !t_slow(st);
+        if (live && (uint32_t) (pos + (int32_t) kBlock) < cur_len) nn = ((nw_in & ~3u) + kBlock) | 1u;
+        else if (pend_ok) nn = ((p_o0 & ~3u) - (uint32_t) base) | 2u;
+      }
+      nw = nn;
+      wait_lgkm0();   /* the reads of the buffer above are done */
+      issue();
+    }
+#endif
 #ifdef RHP_STAMPS
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     RHP_STAMP(t1); acc[0] += t1 - t0; t0 = t1;
@@ -787,7 +895,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     RHP_STAMP(t1); acc[1] += t1 - t0; t0 = t1;
 #endif
     /* [C] */
-    const uint32_t nw_kind = nw & 3u;
+    const uint32_t nw_kind = nw_in & 3u;
     if (nw_kind == 2) {
       cur = pend;
       cur_len = p_o1 - p_o0;
@@ -804,19 +912,23 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const uint32_t head = __builtin_amdgcn_alignbyte(W[0][1], W[0][0], mis);
       cand = head == ('G' | 'E' << 8 | 'T' << 16 | (uint32_t) ' ' << 24) ? 0x40000000u : 0u;
     }
-    if (nw_kind) cur_ptr = nw & ~3u;
+    if (nw_kind) cur_ptr = nw_in & ~3u;
     const bool pend_ready = pend_ok;   /* assigned before this block: p_o0/p_o1 valid */
     /* [D] */
     refill_pend();
 #ifdef RHP_STAMPS
     RHP_STAMP(t1); acc[2] += t1 - t0; t0 = t1;
 #endif
+#if !RHP_EARLY
     /* [E] next window: continuation of cur, else the first window of a ready pend */
     nw = 0;
     if (has && (uint32_t) (pos + (int32_t) kBlock) < cur_len) nw = (cur_ptr + kBlock) | 1u;
     else if (pend_ready) nw = ((p_o0 & ~3u) - (uint32_t) base) | 2u;
     if (kBlock == 128) wait_lgkm0();   /* [A]'s reads of the buffer are done */
     if (kBlock == 128) issue();
+#else
+    (void) pend_ready;
+#endif
     if (!__ballot(has || nw || pend_ok)) break;
 #ifdef RHP_STAMPS
     RHP_STAMP(t1); acc[3] += t1 - t0; t0 = t1;

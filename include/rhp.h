@@ -110,6 +110,53 @@ const char *rhp_kernel_name(void);
 /* Library version string. */
 const char *rhp_version(void);
 
+/*
+ * Batched response serialization: http_write_response (src/reactor/http.c:236-297,
+ * decl http.h:37) for n responses at once, on the device.  Response i is written to
+ * out[out_off[i], out_off[i+1]) byte for byte as the reference appends it to the
+ * stream's output:
+ *   "HTTP/1.1 " status CRLF "Server: *" CRLF "Date: " date CRLF
+ *   "Content-Type: " type CRLF "Content-Length: " decimal(body_len) CRLF
+ *   { name ": " value CRLF }  CRLF body
+ * Every string of a response is a span of the device `arena`.  The date is one
+ * 29-byte IMF-fixdate for the batch (the reactor's cached date; http.c:244 sizes
+ * the response for exactly 29 date bytes, so other lengths are rejected).
+ */
+typedef struct rhp_span {
+  uint32_t off, len;         /* bytes arena[off, off + len) */
+} rhp_span_t;
+
+typedef struct rhp_resp {
+  rhp_span_t status;         /* e.g. "200 OK" */
+  rhp_span_t type;           /* Content-Type value */
+  rhp_span_t body;
+  uint32_t   fields_first;   /* extra fields: fields[fields_first .. + fields_count) */
+  uint32_t   fields_count;
+} rhp_resp_t;
+
+typedef struct rhp_resp_field {
+  rhp_span_t name, value;
+} rhp_resp_field_t;
+
+#define RHP_DATE_LEN 29u
+
+typedef struct rhp_resp_batch {
+  const uint8_t          *arena;    /* device */
+  const rhp_resp_t       *resps;    /* device [n] */
+  const rhp_resp_field_t *fields;   /* device, may be NULL when no response has fields */
+  uint32_t                n;
+  uint32_t                date_len; /* must be RHP_DATE_LEN */
+  const char             *date;     /* host, date_len bytes */
+  uint64_t               *out_off;  /* device [n + 1]: written (exclusive prefix sum of sizes) */
+  uint8_t                *out;      /* device, out_size bytes */
+  uint64_t                out_size; /* when out_off[n] > out_size nothing is written to `out`
+                                       (out_off still holds every size: grow and call again) */
+} rhp_resp_batch_t;
+
+/* Launch status as rhp_parse_batch; three kernels on `stream` (sizes, scan, copy). */
+int rhp_write_responses(const rhp_resp_batch_t *batch, void *stream);
+
+
 #ifdef __cplusplus
 }
 #endif

@@ -51,12 +51,22 @@ class Batch(ctypes.Structure):
 
 
 # exported C-ABI symbols of librhp.so, as declared in include/rhp.h
-RHP_SYMBOLS = ("rhp_parse_batch", "rhp_set_impl", "rhp_kernel_name", "rhp_version")
+RHP_SYMBOLS = ("rhp_parse_batch", "rhp_set_impl", "rhp_kernel_name", "rhp_version", "rhp_write_responses")
 HOST_SYMBOLS = ("rhp_gen_size", "rhp_gen_fill", "rhp_gen_header_bytes", "rhp_splitmix64",
                 "rhp_emu_parse_batch", "rhp_cpu_parse_batch")
 
 _rhp = None
 _host = None
+
+
+class RespBatch(ctypes.Structure):
+    """rhp_resp_batch_t (include/rhp.h): http_write_response over a batch"""
+    _fields_ = [("arena", ctypes.c_void_p), ("resps", ctypes.c_void_p), ("fields", ctypes.c_void_p),
+                ("n", ctypes.c_uint32), ("date_len", ctypes.c_uint32), ("date", ctypes.c_char_p),
+                ("out_off", ctypes.c_void_p), ("out", ctypes.c_void_p), ("out_size", ctypes.c_uint64)]
+
+
+RHP_DATE_LEN = 29
 
 
 def lib() -> ctypes.CDLL:
@@ -72,6 +82,8 @@ def lib() -> ctypes.CDLL:
         _rhp.rhp_set_impl.restype = ctypes.c_int
         _rhp.rhp_kernel_name.restype = ctypes.c_char_p
         _rhp.rhp_version.restype = ctypes.c_char_p
+        _rhp.rhp_write_responses.argtypes = [ctypes.POINTER(RespBatch), ctypes.c_void_p]
+        _rhp.rhp_write_responses.restype = ctypes.c_int
     return _rhp
 
 
@@ -208,3 +220,111 @@ def parse_batch(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: i
         return db.result()
     finally:
         lib().rhp_set_impl(IMPL_DFA)
+
+
+# ---------------------------------------------------------------------------
+# Batched response serialization: http_write_response (src/reactor/http.c:286-297)
+# for n responses on the device (rhp_writer.hip).  A batch is an arena of bytes
+# plus rhp_resp_t records (n x 8 u32: status off,len, type off,len, body off,len,
+# fields_first, fields_count) and rhp_resp_field_t records (m x 4 u32).
+
+RESP_STATUS = (b"200 OK", b"404 Not Found", b"500 Internal Server Error", b"204 No Content",
+               b"101 Switching Protocols")
+RESP_TYPES = (b"text/plain", b"application/json", b"text/html; charset=UTF-8")
+RESP_FIELD_NAMES = (b"Cookie", b"Set-Cookie", b"X-Request-Id", b"Cache-Control")
+DEFAULT_DATE = b"Wed, 16 Aug 2023 10:29:23 GMT"
+
+
+def make_responses(n: int, seed: int, kind: str = "mixed"):
+    """Synthetic response batch (arena, resps, fields).  kind "plaintext": every
+    response is the TechEmpower plaintext reply (200 OK, text/plain,
+    "Hello, World!"); "mixed": seeded statuses/types, 0-3 extra fields, body
+    lengths 0-2000 B with 1 % up to 100 kB (all digit counts of Content-Length)."""
+    rng = np.random.default_rng(seed)
+    parts, pos = [], 0
+
+    def add(b: bytes):
+        nonlocal pos
+        parts.append(b)
+        pos += len(b)
+        return pos - len(b), len(b)
+
+    st = [add(x) for x in RESP_STATUS]
+    ty = [add(x) for x in RESP_TYPES]
+    nm = [add(x) for x in RESP_FIELD_NAMES]
+    resps = np.zeros((n, 8), dtype=np.uint32)
+    fields = []
+    if kind == "plaintext":
+        body = add(b"Hello, World!")
+        resps[:] = [st[0][0], st[0][1], ty[0][0], ty[0][1], body[0], body[1], 0, 0]
+    else:
+        pool = rng.integers(0x20, 0x7F, size=1 << 17, dtype=np.uint8).tobytes()
+        pool_off, _ = add(pool)
+        for i in range(n):
+            s_, t_ = st[int(rng.integers(len(st)))], ty[int(rng.integers(len(ty)))]
+            blen = int(rng.integers(0, 100001)) if rng.random() < 0.01 else int(rng.integers(0, 2001))
+            bo = pool_off + int(rng.integers(0, len(pool) - blen + 1))
+            nf = int(rng.integers(0, 4))
+            first = len(fields)
+            for _ in range(nf):
+                vlen = int(rng.integers(0, 48))
+                fields.append([*nm[int(rng.integers(len(nm)))], pool_off + int(rng.integers(0, 4096)), vlen])
+            resps[i] = [s_[0], s_[1], t_[0], t_[1], bo, blen, first, nf]
+    arena = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+    f = np.array(fields, dtype=np.uint32).reshape(-1, 4) if fields else np.zeros((0, 4), dtype=np.uint32)
+    return arena, resps, f
+
+
+class DeviceResponses:
+    """A response batch resident in HBM and its output (torch tensors as plumbing)."""
+
+    def __init__(self, arena: np.ndarray, resps: np.ndarray, fields: np.ndarray, date: bytes = DEFAULT_DATE,
+                 out_size: int | None = None, device: str = "cuda"):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("no GPU visible: the rhp product path runs on MI355X only")
+        self.n = len(resps)
+        self.date = bytes(date)
+        self.arena = torch.from_numpy(np.ascontiguousarray(arena, dtype=np.uint8)).to(device)
+        self.resps = torch.from_numpy(np.ascontiguousarray(resps, dtype=np.uint32).view(np.int32)).to(device)
+        fl = np.ascontiguousarray(fields, dtype=np.uint32).reshape(-1, 4)
+        self.fields = torch.from_numpy(fl.view(np.int32)).to(device) if len(fl) else None
+        self.out_off = torch.zeros(self.n + 1, dtype=torch.int64, device=device)
+        if out_size is None:   # exact size from the host copy of the records
+            r = np.asarray(resps, dtype=np.uint64).reshape(-1, 8)
+            extra = 0
+            if len(fl):
+                fl64 = fl.astype(np.uint64)
+                per = fl64[:, 1] + fl64[:, 3] + 4
+                extra = int(sum(int(per[a:a + c].sum()) for a, c in zip(r[:, 6], r[:, 7]) if c))
+            digits = np.array([len(str(int(v))) for v in r[:, 5]], dtype=np.uint64)
+            out_size = int((95 + r[:, 1] + r[:, 3] + r[:, 5] + digits).sum()) + extra
+        self.out = torch.zeros(max(out_size, 1), dtype=torch.uint8, device=device)
+        self.out_size = out_size
+
+    def desc(self) -> RespBatch:
+        return RespBatch(self.arena.data_ptr(), self.resps.data_ptr(),
+                         self.fields.data_ptr() if self.fields is not None else None, self.n, len(self.date),
+                         self.date, self.out_off.data_ptr(), self.out.data_ptr(), self.out_size)
+
+    def launch(self, stream=None) -> None:
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        d = self.desc()
+        rc = lib().rhp_write_responses(ctypes.byref(d), ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"rhp_write_responses failed: {rc}")
+
+    def result(self):
+        import torch
+        torch.cuda.synchronize()
+        off = self.out_off.cpu().numpy().view(np.uint64)
+        return self.out.cpu().numpy()[: int(off[-1])], off
+
+
+def write_responses(arena: np.ndarray, resps: np.ndarray, fields: np.ndarray, date: bytes = DEFAULT_DATE):
+    """Serialize a host response batch on the GPU (copies in, one call, copies out):
+    returns (bytes, offsets[n + 1])."""
+    d = DeviceResponses(arena, resps, fields, date)
+    d.launch()
+    return d.result()

@@ -184,3 +184,35 @@ uint64_t ref_phr_batch_mt(const uint8_t *bytes, const uint64_t *offsets, uint32_
   if (checksum) *checksum = sum;
   return (uint64_t) (t1.tv_sec - t0.tv_sec) * 1000000000ull + (uint64_t) (t1.tv_nsec - t0.tv_nsec);
 }
+
+/*
+ * The REAL http_write_response (src/reactor/http.c:286-297) over a batch laid
+ * out as orc_write_responses' arguments: one stream, output_waiting drained
+ * after every response (as test/http.c:143-181 drives it).
+ */
+uint64_t ref_write_responses(const uint8_t *arena, const uint32_t *resps, const uint32_t *fields, uint32_t n,
+                             const uint8_t *date, uint8_t *out, uint64_t *out_off)
+{
+  stream_t s;
+  uint64_t o = 0;
+  http_field_t f[64];
+  stream_construct(&s, NULL, NULL);
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t *r = resps + 8u * i;
+    const uint32_t nf = r[7] < 64 ? r[7] : 64;
+    for (uint32_t k = 0; k < nf; k++) {
+      const uint32_t *x = fields + 4u * (r[6] + k);
+      f[k] = http_field_define(data(arena + x[0], x[1]), data(arena + x[2], x[3]));
+    }
+    http_write_response(&s, data(arena + r[0], r[1]), data(date, 29), data(arena + r[2], r[3]),
+                        data(arena + r[4], r[5]), nf ? f : NULL, nf);
+    data_t d = buffer_data(&s.output_waiting);
+    out_off[i] = o;
+    if (out) memcpy(out + o, data_base(d), data_size(d));
+    o += data_size(d);
+    buffer_clear(&s.output_waiting);
+  }
+  out_off[n] = o;
+  stream_destruct(&s);
+  return o;
+}

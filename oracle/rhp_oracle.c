@@ -22,6 +22,7 @@
 #include "rhp_oracle.h"
 
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -490,4 +491,53 @@ uint64_t orc_phr_batch_mt(const uint8_t *bytes, const uint64_t *offsets, uint32_
     pthread_join(tid[t], NULL);
   clock_gettime(CLOCK_MONOTONIC, &t1);
   return (uint64_t) (t1.tv_sec - t0.tv_sec) * 1000000000ull + (uint64_t) (t1.tv_nsec - t0.tv_nsec);
+}
+
+/*
+ * http_write_response (src/reactor/http.c:286-297) restated for a batch, TEST
+ * INFRASTRUCTURE ONLY.  resps: n x {status off,len, type off,len, body off,len,
+ * fields_first, fields_count}; fields: {name off,len, value off,len}; strings are
+ * spans of `arena`; `date` is 29 bytes.  Response i goes to out[out_off[i],
+ * out_off[i+1]) in the reference's push order: status line (:250-252), Server,
+ * Date, Content-Type, Content-Length fields (:253-256, http_push_field :61-69),
+ * the extra fields (:279-280), the empty line and the body (:257-258).  The length
+ * is printed in decimal (http_u32_sprint :17-44).  out == NULL: offsets only.
+ * Returns the total size.
+ */
+static uint64_t orc_put(uint8_t *out, uint64_t o, const void *src, size_t len)
+{
+  if (out) memcpy(out + o, src, len);
+  return o + len;
+}
+
+uint64_t orc_write_responses(const uint8_t *arena, const uint32_t *resps, const uint32_t *fields, uint32_t n,
+                             const uint8_t *date, uint8_t *out, uint64_t *out_off)
+{
+  uint64_t o = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t *r = resps + 8u * i;
+    char digits[16];
+    const int nd = snprintf(digits, sizeof digits, "%u", r[5]);
+    out_off[i] = o;
+    o = orc_put(out, o, "HTTP/1.1 ", 9);
+    o = orc_put(out, o, arena + r[0], r[1]);
+    o = orc_put(out, o, "\r\nServer: *\r\nDate: ", 19);
+    o = orc_put(out, o, date, 29);
+    o = orc_put(out, o, "\r\nContent-Type: ", 16);
+    o = orc_put(out, o, arena + r[2], r[3]);
+    o = orc_put(out, o, "\r\nContent-Length: ", 18);
+    o = orc_put(out, o, digits, (size_t) nd);
+    o = orc_put(out, o, "\r\n", 2);
+    for (uint32_t f = 0; f < r[7]; f++) {
+      const uint32_t *x = fields + 4u * (r[6] + f);
+      o = orc_put(out, o, arena + x[0], x[1]);
+      o = orc_put(out, o, ": ", 2);
+      o = orc_put(out, o, arena + x[2], x[3]);
+      o = orc_put(out, o, "\r\n", 2);
+    }
+    o = orc_put(out, o, "\r\n", 2);
+    o = orc_put(out, o, arena + r[4], r[5]);
+  }
+  out_off[n] = o;
+  return o;
 }

@@ -74,6 +74,12 @@ uint64_t orc_phr_batch_mt(const uint8_t *bytes, const uint64_t *offsets, uint32_
                           uint32_t max_headers, orc_req_t *reqs, orc_hdr_t *hdrs,
                           int threads, int reps);
 
+/* http_write_response (src/reactor/http.c:286-297) over a batch (rhp_oracle.c) */
+uint64_t orc_write_responses(const uint8_t *arena, const uint32_t *resps, const uint32_t *fields, uint32_t n,
+                             const uint8_t *date, uint8_t *out, uint64_t *out_off);
+uint64_t ref_write_responses(const uint8_t *arena, const uint32_t *resps, const uint32_t *fields, uint32_t n,
+                             const uint8_t *date, uint8_t *out, uint64_t *out_off);
+
 #ifdef __cplusplus
 }
 #endif

@@ -41,6 +41,8 @@ def oracle() -> ctypes.CDLL:
         _orc.orc_http_batch.argtypes = [vp, vp, u32, u32, vp, vp, vp]
         _orc.orc_phr_batch_mt.argtypes = [vp, vp, u32, u32, vp, vp, ctypes.c_int, ctypes.c_int]
         _orc.orc_phr_batch_mt.restype = ctypes.c_uint64
+        _orc.orc_write_responses.argtypes = [vp, vp, vp, u32, ctypes.c_char_p, vp, vp]
+        _orc.orc_write_responses.restype = ctypes.c_uint64
     return _orc
 
 
@@ -56,6 +58,8 @@ def reference():
         vp, u32 = ctypes.c_void_p, ctypes.c_uint32
         _ref.ref_phr_batch.argtypes = [vp, vp, u32, u32, vp, vp]
         _ref.ref_http_batch.argtypes = [vp, vp, u32, u32, vp, vp, vp]
+        _ref.ref_write_responses.argtypes = [vp, vp, vp, u32, ctypes.c_char_p, vp, vp]
+        _ref.ref_write_responses.restype = ctypes.c_uint64
     return _ref
 
 
@@ -166,3 +170,27 @@ def assert_same(got, want, buf=None, off=None, label=""):
         if buf is not None:
             msg.append(f"  bytes {bytes(buf[int(off[i]):int(off[i + 1])])[:300]!r}")
         raise AssertionError("\n".join(msg))
+
+
+def _write_responses(fn, arena, resps, fields, date):
+    """http_write_response over a batch through fn (oracle or reference): (bytes, offsets)"""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    resps = np.ascontiguousarray(resps, dtype=np.uint32)
+    fields = np.ascontiguousarray(fields, dtype=np.uint32).reshape(-1, 4)
+    fp = fields.ctypes.data if len(fields) else None
+    n = len(resps)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    total = fn(arena.ctypes.data, resps.ctypes.data, fp, n, date, None, off.ctypes.data)
+    out = np.zeros(max(int(total), 1), dtype=np.uint8)
+    fn(arena.ctypes.data, resps.ctypes.data, fp, n, date, out.ctypes.data, off.ctypes.data)
+    return out[: int(total)], off
+
+
+def oracle_write_responses(arena, resps, fields, date=rhp.DEFAULT_DATE):
+    return _write_responses(oracle().orc_write_responses, arena, resps, fields, date)
+
+
+def reference_write_responses(arena, resps, fields, date=rhp.DEFAULT_DATE):
+    ref = reference()
+    assert ref is not None, "the compiled reference needs /root/reference"
+    return _write_responses(ref.ref_write_responses, arena, resps, fields, date)

@@ -151,9 +151,13 @@ typedef struct rhp_resp_batch {
   uint8_t                *out;      /* device, out_size bytes */
   uint64_t                out_size; /* when out_off[n] > out_size nothing is written to `out`
                                        (out_off still holds every size: grow and call again) */
+  uint64_t               *work;     /* device scratch, >= RHP_RESP_WORK_WORDS(n) u64 */
 } rhp_resp_batch_t;
 
-/* Launch status as rhp_parse_batch; three kernels on `stream` (sizes, scan, copy). */
+#define RHP_RESP_WORK_WORDS(n) (((uint64_t) (n) + 4095u) / 4096u + 1u)
+
+/* Launch status as rhp_parse_batch; five kernels on `stream` (sizes, three scan
+ * passes, copy). */
 int rhp_write_responses(const rhp_resp_batch_t *batch, void *stream);
 
 

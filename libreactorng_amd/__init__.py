@@ -63,7 +63,8 @@ class RespBatch(ctypes.Structure):
     """rhp_resp_batch_t (include/rhp.h): http_write_response over a batch"""
     _fields_ = [("arena", ctypes.c_void_p), ("resps", ctypes.c_void_p), ("fields", ctypes.c_void_p),
                 ("n", ctypes.c_uint32), ("date_len", ctypes.c_uint32), ("date", ctypes.c_char_p),
-                ("out_off", ctypes.c_void_p), ("out", ctypes.c_void_p), ("out_size", ctypes.c_uint64)]
+                ("out_off", ctypes.c_void_p), ("out", ctypes.c_void_p), ("out_size", ctypes.c_uint64),
+                ("work", ctypes.c_void_p)]
 
 
 RHP_DATE_LEN = 29
@@ -301,11 +302,13 @@ class DeviceResponses:
             out_size = int((95 + r[:, 1] + r[:, 3] + r[:, 5] + digits).sum()) + extra
         self.out = torch.zeros(max(out_size, 1), dtype=torch.uint8, device=device)
         self.out_size = out_size
+        self.work = torch.zeros((self.n + 4095) // 4096 + 1, dtype=torch.int64, device=device)
 
     def desc(self) -> RespBatch:
         return RespBatch(self.arena.data_ptr(), self.resps.data_ptr(),
                          self.fields.data_ptr() if self.fields is not None else None, self.n, len(self.date),
-                         self.date, self.out_off.data_ptr(), self.out.data_ptr(), self.out_size)
+                         self.date, self.out_off.data_ptr(), self.out.data_ptr(), self.out_size,
+                         self.work.data_ptr())
 
     def launch(self, stream=None) -> None:
         import torch

@@ -9,7 +9,9 @@
  *   rhp_resp_size_kernel   thread per response: its size, exactly the sum the
  *                          reference allocates (http.c:244-246, 270-272; the date
  *                          is the fixed 29 bytes the "37" there assumes)
- *   rhp_resp_scan_kernel   one workgroup: in-place exclusive prefix sum -> out_off
+ *   rhp_resp_tile_*_kernel reduce-then-scan over 4096-size tiles (tile sums in the
+ *                          caller's work[], one workgroup scans those, every tile
+ *                          is scanned in place): exclusive prefix sum -> out_off
  *   rhp_resp_write_kernel  wave per response: each segment copied 64 bytes per
  *                          store instruction in the reference's push order
  *                          (http_push_data / http_push_field, http.c:51-69); the
@@ -73,31 +75,85 @@ __global__ __launch_bounds__(256) void rhp_resp_size_kernel(WParams p)
     p.out_off[i + 1] = resp_size(p, p.resps[i]);
 }
 
-/* out_off[1..n] sizes -> out_off[0..n] offsets.  One workgroup: thread t sums a
- * contiguous slice, the slice totals are scanned in LDS, then every slice is
- * rewritten with its running offsets. */
-__global__ __launch_bounds__(1024) void rhp_resp_scan_kernel(uint64_t *a, uint32_t n)
+/* out_off[1..n] sizes -> out_off[0..n] offsets, reduce-then-scan over tiles of
+ * kTile sizes: tile sums into work[], one workgroup scans work[] (exclusive),
+ * then every tile is scanned in place with its carry.  Loads and stores are
+ * coalesced; within a workgroup a thread scans 4 consecutive sizes, a wave its
+ * 64 threads through shuffles, the workgroup its 16 waves through LDS. */
+constexpr uint32_t kTile = 4096;   /* 1024 threads x 4 */
+
+__device__ __forceinline__ unsigned long long wave_incl_scan(unsigned long long v, uint32_t lane)
 {
-  __shared__ uint64_t part[1024];
-  const uint32_t t = threadIdx.x;
-  const uint32_t per = (n + 1023u) / 1024u;
-  const uint64_t lo = 1 + (uint64_t) t * per, hi = min(lo + per, (uint64_t) n + 1);
-  uint64_t s = 0;
-  for (uint64_t k = lo; k < hi; k++) s += a[k];
-  part[t] = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long u = __shfl_up(v, o);
+    if ((int) lane >= o) v += u;
+  }
+  return v;
+}
+
+/* inclusive scan of one value per thread over a 1024-thread workgroup */
+__device__ __forceinline__ unsigned long long block_incl_scan(unsigned long long v, unsigned long long *part)
+{
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  v = wave_incl_scan(v, lane);
+  if (lane == 63) part[w] = v;
   __syncthreads();
-  for (uint32_t d = 1; d < 1024u; d <<= 1) {
-    const uint64_t v = t >= d ? part[t - d] : 0;
-    __syncthreads();
-    part[t] += v;
+  if (w == 0) {
+    unsigned long long x = lane < 16 ? part[lane] : 0;
+    x = wave_incl_scan(x, lane);
+    if (lane < 16) part[lane] = x;
+  }
+  __syncthreads();
+  return v + (w ? part[w - 1] : 0);
+}
+
+__global__ __launch_bounds__(1024) void rhp_resp_tile_sum_kernel(const uint64_t *a, uint32_t n, uint64_t *work)
+{
+  __shared__ unsigned long long part[16];
+  const uint64_t lo = 1 + (uint64_t) blockIdx.x * kTile, hi = min(lo + kTile, (uint64_t) n + 1);
+  unsigned long long s = 0;
+  for (uint64_t k = lo + threadIdx.x; k < hi; k += 1024) s += a[k];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < 16; w++) t += part[w];
+    work[blockIdx.x] = t;
+  }
+}
+
+/* work[0..tiles) -> exclusive offsets (one workgroup, 1024 per round) */
+__global__ __launch_bounds__(1024) void rhp_resp_top_scan_kernel(uint64_t *work, uint32_t tiles)
+{
+  __shared__ unsigned long long part[16];
+  unsigned long long carry = 0;
+  for (uint32_t b = 0; b < tiles; b += 1024) {
+    const uint32_t k = b + threadIdx.x;
+    const unsigned long long v = k < tiles ? work[k] : 0;
+    const unsigned long long inc = block_incl_scan(v, part);
+    if (k < tiles) work[k] = carry + inc - v;
+    carry += part[15];   /* the round's total */
     __syncthreads();
   }
-  uint64_t base = t ? part[t - 1] : 0;
-  for (uint64_t k = lo; k < hi; k++) {
-    base += a[k];
-    a[k] = base;
+}
+
+__global__ __launch_bounds__(1024) void rhp_resp_tile_scan_kernel(uint64_t *a, uint32_t n, const uint64_t *work)
+{
+  __shared__ unsigned long long part[16];
+  const uint64_t base = 1 + (uint64_t) blockIdx.x * kTile + 4u * threadIdx.x, end = (uint64_t) n + 1;
+  unsigned long long x[4], s = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    x[q] = base + q < end ? a[base + q] : 0;
+    s += x[q];
+    x[q] = s;   /* thread-local inclusive */
   }
-  if (t == 0) a[0] = 0;
+  const unsigned long long before = block_incl_scan(s, part) - s + work[blockIdx.x];
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    if (base + q < end) a[base + q] = before + x[q];
+  if (blockIdx.x == 0 && threadIdx.x == 0) a[0] = 0;
 }
 
 /* one segment of a response, 64 bytes per store instruction */
@@ -156,6 +212,7 @@ extern "C" int rhp_write_responses(const rhp_resp_batch_t *b, void *stream)
   if (!b->out_off || !b->date || b->date_len != RHP_DATE_LEN) return -22;
   if (b->n > 0 && (!b->arena || !b->resps)) return -22;
   if (!b->out && b->out_size != 0) return -22;
+  if (b->n > 0 && !b->work) return -22;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (g_writer_cus == 0) {
     int dev = 0;
@@ -178,7 +235,11 @@ extern "C" int rhp_write_responses(const rhp_resp_batch_t *b, void *stream)
   uint32_t g1 = (b->n + 255u) / 256u;
   if (g1 > cap) g1 = cap;
   hipLaunchKernelGGL(rhp_resp_size_kernel, dim3(g1), dim3(256), 0, s, p);
-  hipLaunchKernelGGL(rhp_resp_scan_kernel, dim3(1), dim3(1024), 0, s, b->out_off, b->n);
+  const uint32_t tiles = (b->n + kTile - 1u) / kTile;
+  hipLaunchKernelGGL(rhp_resp_tile_sum_kernel, dim3(tiles), dim3(1024), 0, s, b->out_off, b->n, b->work);
+  hipLaunchKernelGGL(rhp_resp_top_scan_kernel, dim3(1), dim3(1024), 0, s, b->work, tiles);
+  hipLaunchKernelGGL(rhp_resp_tile_scan_kernel, dim3(tiles), dim3(1024), 0, s, b->out_off, b->n,
+                     (const uint64_t *) b->work);
   uint32_t g3 = (b->n + 3u) / 4u;   /* 4 waves per workgroup, a wave per response */
   if (g3 > cap * 4u) g3 = cap * 4u;
   hipLaunchKernelGGL(rhp_resp_write_kernel, dim3(g3), dim3(256), 0, s, p);

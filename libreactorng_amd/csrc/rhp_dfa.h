@@ -285,6 +285,19 @@ enum : uint32_t {
   kTable2Bytes = kRows2 * 256u
 };
 static_assert(kClassRow < kRows2 && state2(kClassRow) >= S_COUNT, "class row is a hole");
+
+/*
+ * Pair codes by two lookups instead of arithmetic (the kernel's RHP_CODE2 form):
+ *   r    = T[kClassRowR * 256 + b1]     the row of class(b1): code_row(class(b1))
+ *   code = T[r * 256 + b0]              = class(b0) * 16 + class(b1)
+ * so a pair costs two address v_perms and no packing ops.  The rows live in
+ * holes of the pair table (plain-state rows 4s+2, 4s+3, s >= 8, no state uses).
+ */
+RHP_DHD constexpr uint32_t code_row(uint32_t k) { return 4u * (9u + k) + 2u; }   /* k < kClasses */
+enum : uint32_t { kClassRowR = kClassRow + 1u };
+static_assert(kClassRowR < kRows2 && state2(kClassRowR) >= S_COUNT, "class-row row is a hole");
+static_assert(code_row(kClasses - 1u) < kRows2 && state2(code_row(0)) >= S_COUNT &&
+              state2(code_row(kClasses - 1u)) >= S_COUNT, "code rows are holes");
 static_assert(kRows2 <= 256u, "indices are bytes");
 
 RHP_DHD constexpr bool is_done2(uint32_t i) { return state2(i) == S_DONE || state2(i) == S_DONE_E; }
@@ -315,6 +328,9 @@ constexpr Table2 make_table2()
     }
   }
   for (uint32_t c = 0; c < 256; c++) t.b[kClassRow * 256u + c] = (uint8_t) byte_class(c);
+  for (uint32_t c = 0; c < 256; c++) t.b[kClassRowR * 256u + c] = (uint8_t) code_row(byte_class(c));
+  for (uint32_t k = 0; k < kClasses; k++)
+    for (uint32_t c = 0; c < 256; c++) t.b[code_row(k) * 256u + c] = (uint8_t) (byte_class(c) * 16u + k);
   return t;
 }
 

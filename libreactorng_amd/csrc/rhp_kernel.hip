@@ -61,6 +61,9 @@ using namespace rhp;
 #ifndef RHP_EARLY
 #define RHP_EARLY 0     /* issue the next window before the decode (128-B windows); measured no gain, profiles/r01/v9 */
 #endif
+#ifndef RHP_CODE2
+#define RHP_CODE2 1     /* pair codes by two table lookups (rhp_dfa.h code_row) */
+#endif
 #ifndef RHP_SKIP
 #define RHP_SKIP 0   /* pair DFA: skip chunks of run bytes wave-uniformly (rhp_dfa.h runs_exact); measured no gain, profiles/r01/v9 */
 #endif
@@ -731,6 +734,50 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
           asm("v_alignbit_b32 %0, %1, %0, 1" : "+v"(evw[q >> 1]) : "v"(st));
         }
         __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+#elif RHP_CODE2
+  /* pair codes by two lookups (rhp_dfa.h code_row): A = the row of class(b1),
+   * B = class(b0) * 16 + class(b1) from that row; 2 VALU per pair for the codes
+   * instead of 2 class addresses + 2 packing ops.  Chunk q+1's A reads are issued
+   * before chunk q's chain, its B reads (which wait on A) after half the chain. */
+  auto codes_a = [&](const u32x4 &chunk, uint32_t (&r)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      r[j] = lds_u8(__builtin_amdgcn_perm(kClassRowR, chunk[j >> 1], 0x0c0c0400u | (uint32_t) (2 * (j & 1) + 1)));
+  };
+  auto codes_b = [&](const u32x4 &chunk, const uint32_t (&r)[8], uint32_t (&c)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      c[j] = lds_u8(__builtin_amdgcn_perm(r[j], chunk[j >> 1], 0x0c0c0400u | (uint32_t) (2 * (j & 1))));
+  };
+  auto steps4 = [&](const uint32_t (&c)[8], int j0, uint32_t &ev) {
+#pragma unroll
+    for (int j = j0; j < j0 + 4; j++) {
+      st = lds_u8(__builtin_amdgcn_perm(st, c[j], 0x0c0c0400u));
+      ev_shift2(ev, st);
+    }
+  };
+  auto steps_chunks = [&](const u32x4 *Wc, int nchunks, uint32_t *evw) {
+    uint32_t c[8], r[8];
+    codes_a(Wc[0], r);
+    codes_b(Wc[0], r, c);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      if (q >= nchunks) break;
+      uint32_t cn[8];
+      if (q + 1 < nchunks) codes_a(Wc[q + 1], r);
+      __builtin_amdgcn_sched_barrier(0);
+      steps4(c, 0, evw[q >> 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (q + 1 < nchunks) codes_b(Wc[q + 1], r, cn);
+      __builtin_amdgcn_sched_barrier(0);
+      steps4(c, 4, evw[q >> 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (q + 1 < nchunks) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) c[j] = cn[j];
       }
     }
   };

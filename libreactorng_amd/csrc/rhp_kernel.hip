@@ -61,6 +61,9 @@ using namespace rhp;
 #ifndef RHP_EARLY
 #define RHP_EARLY 0     /* issue the next window before the decode (128-B windows); measured no gain, profiles/r01/v9 */
 #endif
+#ifndef RHP_PEND2
+#define RHP_PEND2 0     /* two pending requests per lane (see promote); measured worse, profiles/r01/v9 */
+#endif
 #ifndef RHP_CODE2
 #define RHP_CODE2 1     /* pair codes by two table lookups (rhp_dfa.h code_row) */
 #endif
@@ -119,6 +122,7 @@ enum : uint32_t {
 };
 static_assert(kBlock == 64 || kBlock == 128, "64- or 128-byte windows");
 static_assert(!RHP_EARLY || kBlock == 128, "early issue needs whole-line windows");
+static_assert(!(RHP_EARLY && RHP_PEND2), "the early issue predicts the single-pend switch");
 static_assert(idx2(S_DONE, 0) == kPark && idx8(S_DONE) == kPark, "parked lanes sit in DONE");
 
 /* LDS byte address of part q (16 B) of lane w's window inside the staging
@@ -475,6 +479,17 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   bool pend_ok = false;                /* pend: the lane's next request */
   uint32_t pend = 0;
   uint32_t pend_o0 = 0, pend_o1 = 0;   /* low dwords of offsets[pend], offsets[pend+1] as loaded */
+#if RHP_PEND2
+  /* a second pending request behind pend: refills fill `back`, and a switch
+   * promotes it to pend at once, its offsets loaded an iteration earlier, so a
+   * lane whose request fits one window starts the next one's window right away
+   * instead of idling an iteration while the new pend's offsets arrive */
+  bool back_ok = false;
+  uint32_t back = 0, back_o0 = 0, back_o1 = 0;
+#define RHP_SLOT_OK back_ok
+#else
+#define RHP_SLOT_OK pend_ok
+#endif
   uint32_t nw = 0;                     /* next window: byte offset from base | kind (0 none, 1
                                           continuation, 2 first window of pend); windows are 4-aligned */
   /* the window in registers: half of a 64-B window (the other half is read
@@ -486,16 +501,35 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   /* give every lane without a pending request one from the pool; the offsets
    * loads are only consumed at the top of the next block */
   auto take = [&](uint32_t i) {
-    pend = i;
     /* only the low dwords: a batch is below 4 GiB, so offsets relative to
      * `base` and lengths are exact modulo 2^32 */
-    const uint32_t *o = reinterpret_cast<const uint32_t *>(p.offsets + pend);
+    const uint32_t *o = reinterpret_cast<const uint32_t *>(p.offsets + i);
+#if RHP_PEND2
+    back = i;
+    back_o0 = *GLOBAL(const uint32_t, o);
+    back_o1 = *GLOBAL(const uint32_t, o + 2);
+    back_ok = true;
+#else
+    pend = i;
     pend_o0 = *GLOBAL(const uint32_t, o);
     pend_o1 = *GLOBAL(const uint32_t, o + 2);
     pend_ok = true;
+#endif
+  };
+  /* back -> pend (RHP_PEND2); call only after a wait_vm0 that covers back's loads */
+  auto promote = [&]() {
+#if RHP_PEND2
+    if (!pend_ok && back_ok) {
+      pend = back;
+      pend_o0 = back_o0;
+      pend_o1 = back_o1;
+      pend_ok = true;
+      back_ok = false;
+    }
+#endif
   };
   auto refill_pend = [&]() {
-    uint64_t want = __ballot(!pend_ok);
+    uint64_t want = __ballot(!RHP_SLOT_OK);
     if (!want || (pool_dry && list_dry)) return;
     if (!list_dry && !first_iter) {   /* the long list first */
       const uint32_t cnt = (uint32_t) __popcll(want);
@@ -505,8 +539,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const uint32_t nl = min(*list_n, (uint32_t) kListCap);
       if (b0 + cnt >= nl) list_dry = true;
       const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
-      if (!pend_ok && b0 + rank < nl) take(wg_lo + long_list[b0 + rank]);
-      want = __ballot(!pend_ok);
+      if (!RHP_SLOT_OK && b0 + rank < nl) take(wg_lo + long_list[b0 + rank]);
+      want = __ballot(!RHP_SLOT_OK);
     }
     /* the range in order, skipping the listed requests (a few rounds at most) */
     while (want && !pool_dry) {
@@ -517,8 +551,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (b0 + cnt >= wg_hi) pool_dry = true;
       const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
       const uint32_t i = b0 + rank, k = i - wg_lo;
-      if (!pend_ok && i < wg_hi && !(order_on && ((long_bits[k >> 5] >> (k & 31)) & 1u))) take(i);
-      want = __ballot(!pend_ok);
+      if (!RHP_SLOT_OK && i < wg_hi && !(order_on && ((long_bits[k >> 5] >> (k & 31)) & 1u))) take(i);
+      want = __ballot(!RHP_SLOT_OK);
     }
   };
 
@@ -882,11 +916,15 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * Issue the first windows, then (while they land) the long-request scan; the
    * barrier makes the list complete before any wave's next refill. */
   wait_vm0();   /* the pending offsets */
+  promote();
   nw = pend_ok ? ((pend_o0 & ~3u) - (uint32_t) base) | 2u : 0u;
   issue();
   if (order_on) scan_long();
   __syncthreads();
   first_iter = false;
+#if RHP_PEND2
+  refill_pend();   /* back, after the long list is complete */
+#endif
 
 #ifdef RHP_STAMPS
   unsigned long long t0 = 0, t1 = 0, acc[6] = {0, 0, 0, 0, 0, 0}, t_loop = 0;
@@ -960,7 +998,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       cand = head == ('G' | 'E' << 8 | 'T' << 16 | (uint32_t) ' ' << 24) ? 0x40000000u : 0u;
     }
     if (nw_kind) cur_ptr = nw_in & ~3u;
-    const bool pend_ready = pend_ok;   /* assigned before this block: p_o0/p_o1 valid */
+    promote();
+    const bool pend_ready = pend_ok;   /* assigned before this block: its offsets are valid */
+    const uint32_t r_o0 = RHP_PEND2 ? pend_o0 : p_o0;
     /* [D] */
     refill_pend();
 #ifdef RHP_STAMPS
@@ -970,13 +1010,14 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     /* [E] next window: continuation of cur, else the first window of a ready pend */
     nw = 0;
     if (has && (uint32_t) (pos + (int32_t) kBlock) < cur_len) nw = (cur_ptr + kBlock) | 1u;
-    else if (pend_ready) nw = ((p_o0 & ~3u) - (uint32_t) base) | 2u;
+    else if (pend_ready) nw = ((r_o0 & ~3u) - (uint32_t) base) | 2u;
     if (kBlock == 128) wait_lgkm0();   /* [A]'s reads of the buffer are done */
     if (kBlock == 128) issue();
 #else
     (void) pend_ready;
+    (void) r_o0;
 #endif
-    if (!__ballot(has || nw || pend_ok)) break;
+    if (!__ballot(has || nw || pend_ok || RHP_SLOT_OK)) break;
 #ifdef RHP_STAMPS
     RHP_STAMP(t1); acc[3] += t1 - t0; t0 = t1;
 #endif

@@ -793,6 +793,52 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       ev_shift2(ev, st);
     }
   };
+#if RHP_SKIP
+  /* run skipping (see the RHP_SKIP form below) on the two-lookup codes */
+  auto run16 = [&](const u32x4 &c) -> bool {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      const uint32_t x = c[d], y = x ^ 0x7f7f7f7fu;
+      acc |= ((x - 0x21212121u) & ~x) | ((y - 0x01010101u) & ~y);
+    }
+    return (acc & 0x80808080u) == 0;
+  };
+  auto steps_chunks = [&](const u32x4 *Wc, int nchunks, uint32_t *evw) {
+    uint32_t c[8], r[8];
+    bool ahead = false;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      if (q >= nchunks) break;
+      const uint32_t s = st & ~1u;
+      const bool in_run = s == 4u * S_PATH || s == 4u * S_VALUE || s == 4u * S_VWS;
+      if (!__builtin_amdgcn_ballot_w64(!in_run) && !__builtin_amdgcn_ballot_w64(!run16(Wc[q]))) {
+        st = s == 4u * S_PATH ? 4u * S_PATH : 4u * S_VALUE;
+        evw[q >> 1] >>= 16;
+        ahead = false;
+        continue;
+      }
+      if (!ahead) {
+        codes_a(Wc[q], r);
+        codes_b(Wc[q], r, c);
+      }
+      uint32_t cn[8];
+      if (q + 1 < nchunks) codes_a(Wc[q + 1], r);
+      __builtin_amdgcn_sched_barrier(0);
+      steps4(c, 0, evw[q >> 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (q + 1 < nchunks) codes_b(Wc[q + 1], r, cn);
+      __builtin_amdgcn_sched_barrier(0);
+      steps4(c, 4, evw[q >> 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (q + 1 < nchunks) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) c[j] = cn[j];
+      }
+      ahead = q + 1 < nchunks;
+    }
+  };
+#else
   auto steps_chunks = [&](const u32x4 *Wc, int nchunks, uint32_t *evw) {
     uint32_t c[8], r[8];
     codes_a(Wc[0], r);
@@ -815,6 +861,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       }
     }
   };
+#endif
 #elif RHP_SKIP
   /* 16 bytes are all run bytes (rhp_dfa.h c_run: > 0x20 and not DEL).  SWAR,
    * exact as an existence test: (x - 0x21..) & ~x has a byte's top bit set for

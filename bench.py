@@ -6,19 +6,29 @@ Metric (BASELINE.json): "GiB/s device-resident batched HTTP/1.1 request parse,
 batch of synthetic requests already resident in HBM.
 
 Workloads:
-  N=1  config 2: 1M x 256 B GET, 4 headers, max_headers 16 (phr mode)
+  N=1  config 2: 1M x 256 B GET, 4 headers, max_headers 16 (phr mode) -> `value`;
+       configs 3 and 5 are timed too, in `extra_configs`
   N>1  config 4: config 2's generator sharded evenly, 1M requests per GPU
        (8M at N=8), no collective on the data path -> weak scaling
-  --config zipf|post are the other BASELINE configs (parity-tested; optional lines)
+
+Launch: `python bench.py --gpus N` starts N rank processes itself (one per GPU,
+before any GPU call, device = LOCAL_RANK); under torch.distributed.run the ranks
+come from RANK / LOCAL_RANK / WORLD_SIZE, which must equal --gpus.
 
 Inputs rotate over >= 4 resident copies (>= 1 GiB) so every launch reads HBM,
 not the 256 MiB Infinity Cache.  value = algorithmic bytes (header-section bytes
-the reference reads) of all ranks / max-over-ranks time, in GiB/s.
+the reference reads) of all ranks / max-over-ranks time, GiB/s.
 
 The roofline leg times the kernel with HIP events on the stream it is launched
 on (torch's current stream is passed to the C-ABI).  cpu_baseline times the
-oracle restatement (oracle/liboracle.so, "port") on rank 0, N=1 only, on a
-bounded sample of the same workload.
+reference's own parser (oracle/_ref/libref.so: the reference compiled from
+/root/reference in the dev container; it travels to the GPU box as a built
+library) on rank 0, N=1 only, on a bounded sample of each workload, at 1
+thread and at all CPUs this process may use.
+
+--device cpu runs the same harness with the CPU emulation of the kernel
+(rhp_emu_parse_batch) instead of the GPU: a test of the launcher, sharding and
+reduction on machines without a GPU, never a measurement.
 """
 from __future__ import annotations
 
@@ -26,6 +36,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,6 +48,7 @@ sys.path.insert(0, ROOT)
 
 import libreactorng_amd as rhp  # noqa: E402
 
+METRIC = "GiB/s device-resident batched HTTP/1.1 request parse, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E, GB/s (MI355X_MICROARCH.md chip table)
 CONFIGS = {
     "get256": dict(gen=rhp.GEN_GET256, seed=0x5EED0002, maxh=16, mode=rhp.MODE_PHR, per_gpu=1 << 20,
@@ -53,154 +66,304 @@ def shard_range(n_total: int, rank: int, world: int):
 
 
 def traffic_from_profile(config_key: str):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary, if any
-    (tools/pmc_traffic.py writes it; FETCH_SIZE doubled on gfx950)."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this
+    kernel (profiles/pmc_traffic.json: FETCH_SIZE x 2 on gfx950 + WRITE_SIZE),
+    with the profile it came from; (None, None) if absent."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        d = json.load(open(path))
-        return d.get(config_key, {}).get("hbm_bytes_per_launch")
+        d = json.load(open(path)).get(config_key, {})
+        return d.get("hbm_bytes_per_launch"), d.get("source")
     except Exception:
-        return None
+        return None, None
 
 
-def cpu_baseline(cfg, seconds: float = 12.0):
-    """The reference CPU parser on the host cores, on a bounded sample of the workload.
+def cpu_info():
+    """CPU model and the CPUs this process may use (affinity, cgroup quota)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    usable = affinity if quota is None else max(1, min(affinity, int(quota)))
+    return model, affinity, quota, usable
 
-    Prefers the real reference (phr_parse_request compiled from the reference's
-    sources with its own -O3 flags into oracle/_ref/libref.so by oracle/Makefile,
-    kind "reference"); falls back to the from-scratch restatement (kind "port")
-    when that library is absent (it is built only where /root/reference exists)."""
+
+def cpu_baseline(keys, seconds: float = 5.0):
+    """The reference CPU parser on the host cores, per config, at 1 thread and
+    at every usable CPU, on a bounded sample (2^18 requests) of each workload.
+
+    The timed code is the reference's own phr_parse_request (phr configs) or
+    http_read_request (config 5), compiled from /root/reference with its -O3
+    flags into oracle/_ref/libref.so by oracle/Makefile in the dev container
+    (kind "reference").  Without that library the from-scratch restatement
+    oracle/liboracle.so is timed instead (kind "port")."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from oracle_util import LIBREF, ORC_HDR, ORC_REQ, oracle
-    n = 1 << 18
-    buf, off = rhp.generate(cfg["gen"], n, cfg["seed"])
-    hb = rhp.header_bytes(cfg["gen"], n, cfg["seed"])
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    if os.path.exists(LIBREF):
-        ref = ctypes.CDLL(LIBREF)
-        ref.ref_phr_batch_mt.restype = ctypes.c_uint64
-        ref.ref_phr_batch_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
-                                         ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
-        chk = ctypes.c_long(0)
-        run = lambda t, reps: ref.ref_phr_batch_mt(buf.ctypes.data, off.ctypes.data, n, cfg["maxh"], t, reps,
-                                                   ctypes.byref(chk))
-        kind, what = "reference", ("phr_parse_request of the reference (src/picohttpparser/picohttpparser.c, "
-                                   "gcc -O3 -march=x86-64-v3 as its Makefile.am:61 builds it, SSE4.2 path)")
-    else:
-        o = oracle()
-        reqs = np.zeros(n, dtype=ORC_REQ)
-        hdrs = np.zeros((n, cfg["maxh"]), dtype=ORC_HDR)
-        run = lambda t, reps: o.orc_phr_batch_mt(buf.ctypes.data, off.ctypes.data, n, cfg["maxh"],
-                                                 reqs.ctypes.data, hdrs.ctypes.data, t, reps)
-        kind, what = "port", "oracle/rhp_oracle.c phr_parse_request restatement (gcc -O3 -march=x86-64-v3)"
+    from oracle_util import LIBREF, ORC_HDR, ORC_HTTP, ORC_REQ, oracle
+    model, affinity, quota, usable = cpu_info()
+    have_ref = os.path.exists(LIBREF)
+    ref = ctypes.CDLL(LIBREF) if have_ref else None
+    vp, u32, c_int = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
     out = {}
-    for t in sorted({1, threads}):
-        run(t, 1)
-        one = run(t, 1) / 1e9
-        reps = max(1, int(seconds / 2 / max(one, 1e-6)))
-        ns = run(t, reps)
-        out[t] = (hb * reps / (ns / 1e9) / 2 ** 30, reps)
-    v, reps = out[threads]
-    return {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "value_1_thread": round(out[1][0], 3),
-            "sample": f"{what}; {n} requests of the same workload x {reps} passes, {threads} pthreads"}
+    for key in keys:
+        cfg = CONFIGS[key]
+        n = 1 << 18
+        buf, off = rhp.generate(cfg["gen"], n, cfg["seed"])
+        hb = rhp.header_bytes(cfg["gen"], n, cfg["seed"])
+        chk = ctypes.c_long(0)
+        if have_ref:
+            fn = ref.ref_http_batch_mt if cfg["mode"] == rhp.MODE_HTTP else ref.ref_phr_batch_mt
+            fn.restype = ctypes.c_uint64
+            fn.argtypes = [vp, vp, u32, u32, c_int, c_int, vp]
+            run = lambda t, reps, fn=fn, buf=buf, off=off, cfg=cfg: fn(buf.ctypes.data, off.ctypes.data, n,
+                                                                       cfg["maxh"], t, reps, ctypes.byref(chk))
+            what = ("http_read_request" if cfg["mode"] == rhp.MODE_HTTP else "phr_parse_request") + \
+                " of the reference (compiled from /root/reference by oracle/Makefile, gcc -O3 -march=x86-64-v3, " \
+                "SSE4.2 path)"
+            kind = "reference"
+        else:
+            o = oracle()
+            reqs = np.zeros(n, dtype=ORC_REQ)
+            hdrs = np.zeros((n, cfg["maxh"]), dtype=ORC_HDR)
+            if cfg["mode"] == rhp.MODE_HTTP:
+                http = np.zeros(n, dtype=ORC_HTTP)
+
+                def run(t, reps, buf=buf, off=off, cfg=cfg):
+                    t0 = time.perf_counter_ns()
+                    for _ in range(reps):
+                        o.orc_http_batch(buf.ctypes.data, off.ctypes.data, n, cfg["maxh"], reqs.ctypes.data,
+                                         hdrs.ctypes.data, http.ctypes.data)
+                    return time.perf_counter_ns() - t0
+            else:
+                run = lambda t, reps, buf=buf, off=off, cfg=cfg: o.orc_phr_batch_mt(
+                    buf.ctypes.data, off.ctypes.data, n, cfg["maxh"], reqs.ctypes.data, hdrs.ctypes.data, t, reps)
+            what, kind = "oracle/rhp_oracle.c restatement (gcc -O3 -march=x86-64-v3)", "port"
+        res = {}
+        for t in sorted({1, usable}):
+            if kind == "port" and cfg["mode"] == rhp.MODE_HTTP and t > 1:
+                continue
+            run(t, 1)
+            one = run(t, 1) / 1e9
+            reps = max(1, int(seconds / 2 / max(one, 1e-6)))
+            ns = run(t, reps)
+            res[t] = (hb * reps / (ns / 1e9) / 2 ** 30, reps)
+        top = max(res)
+        out[key] = {"value": round(res[top][0], 3), "cores": top, "value_1_thread": round(res[1][0], 3),
+                    "sample": f"{what}; {n} requests of {cfg['name']} x {res[top][1]} passes"}
+    main_key = keys[0]
+    line = {"value": out[main_key]["value"], "unit": "GiB/s", "cores": out[main_key]["cores"], "kind": kind,
+            "value_1_thread": out[main_key]["value_1_thread"], "sample": out[main_key]["sample"],
+            "cpu_model": model, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "per_config": {k: {kk: v for kk, v in d.items() if kk != "sample"} for k, d in out.items()},
+            "note": "timed binary: the reference built from its own sources in the dev container "
+                    "(oracle/_ref/libref.so), shipped to this box as a library" if kind == "reference" else
+                    "timed binary: the from-scratch oracle restatement"}
+    return line
 
 
-def main():
+# ---------------------------------------------------------------- launcher
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(argv, n: int) -> int:
+    """Start n rank processes of this script (before any GPU call here) and
+    return the worst exit status.  Rank r drives GPU r (LOCAL_RANK)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    codes = [p.wait() for p in procs]
+    return max(codes, key=abs)
+
+
+# ---------------------------------------------------------------- timing
+
+class GpuRunner:
+    """A config's shard resident in HBM (rotated copies), launched on torch's
+    current stream and timed with HIP events on that stream."""
+
+    def __init__(self, cfg, lo, hi, copies):
+        import torch
+        self.torch = torch
+        buf, off = rhp.generate(cfg["gen"], hi - lo, cfg["seed"], lo=lo)
+        self.copies = [rhp.DeviceBatch(buf, off, cfg["maxh"], cfg["mode"]) for _ in range(max(1, copies))]
+        for c in self.copies[1:]:   # one set of output records
+            c.reqs, c.hdrs, c.http = self.copies[0].reqs, self.copies[0].hdrs, self.copies[0].http
+        self.stream = torch.cuda.current_stream()
+
+    def step(self, k):
+        self.copies[k % len(self.copies)].launch(self.stream)
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def timed(self, steps):
+        """(wall seconds, mean launch ms from HIP events on the launch stream)"""
+        torch = self.torch
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(self.stream)
+        for k in range(steps):
+            self.step(k)
+        ev1.record(self.stream)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, ev0.elapsed_time(ev1) / steps
+
+    def ok_fraction(self):
+        res = self.copies[0].result()
+        return float((res.reqs["ret"] > 0).mean()) if len(res.reqs) else 1.0
+
+
+class EmuRunner:
+    """--device cpu: the kernel's CPU emulation (harness tests only)."""
+
+    def __init__(self, cfg, lo, hi, copies):
+        self.buf, self.off = rhp.generate(cfg["gen"], hi - lo, cfg["seed"], lo=lo)
+        self.cfg = cfg
+        self.res = None
+
+    def step(self, k):
+        self.res, _ = rhp.emulate(self.buf, self.off, self.cfg["maxh"], self.cfg["mode"])
+
+    def sync(self):
+        pass
+
+    def timed(self, steps):
+        t0 = time.perf_counter()
+        for k in range(steps):
+            self.step(k)
+        wall = time.perf_counter() - t0
+        return wall, wall * 1e3 / max(steps, 1)
+
+    def ok_fraction(self):
+        return float((self.res.reqs["ret"] > 0).mean()) if self.res is not None and len(self.res.reqs) else 1.0
+
+
+def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
+    cfg = CONFIGS[key]
+    n_total = per_gpu * world
+    lo, hi = shard_range(n_total, rank, world)
+    alg_bytes = rhp.header_bytes(cfg["gen"], hi - lo, cfg["seed"], lo=lo)
+    runner = (EmuRunner if args.device == "cpu" else GpuRunner)(cfg, lo, hi, args.copies)
+    for k in range(warmup):
+        runner.step(k)
+    runner.sync()
+    ok_frac = runner.ok_fraction()
+    if dist is not None:
+        dist.barrier()
+    runner.sync()
+    wall, kern_ms = runner.timed(steps)
+    if dist is not None:
+        dist.barrier()
+    total_alg = float(alg_bytes)
+    if dist is not None:
+        import torch
+        t = torch.tensor([wall, kern_ms], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, kern_ms = float(t[0]), float(t[1])
+        tb = torch.tensor([float(alg_bytes)], dtype=torch.float64)
+        dist.all_reduce(tb)
+        total_alg = float(tb[0])
+    return dict(cfg=cfg, lo=lo, hi=hi, n_total=n_total, alg_bytes=alg_bytes, total_alg=total_alg, wall=wall,
+                kern_ms=kern_ms, ok_frac=ok_frac, steps=steps, warmup=warmup)
+
+
+def roofline(r, key):
+    achieved = r["alg_bytes"] / (r["kern_ms"] * 1e-3) / 1e9
+    traffic, source = traffic_from_profile(key)
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": source,
+            "kernel_ms": round(r["kern_ms"], 4), "algorithmic_bytes_per_launch": int(r["alg_bytes"])}
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="get256", choices=sorted(CONFIGS))
+    ap.add_argument("--extra", default="auto", choices=["auto", "none"],
+                    help="auto: at N=1 also time configs 3 and 5 (extra_configs)")
+    ap.add_argument("--extra-steps", type=int, default=20)
     ap.add_argument("--copies", type=int, default=4)
+    ap.add_argument("--per-gpu", type=int, default=0, help="requests per GPU (default: the config's 1M)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--impl", type=int, default=rhp.IMPL_DFA)
-    args = ap.parse_args()
+    ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
+    argv = sys.argv[1:] if argv is None else argv
+    args = ap.parse_args(argv)
 
-    import torch
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(argv, args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        world = max(world, 1)
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+
+    dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")  # control plane only: no data-path collective
-    torch.cuda.set_device(local)
-    cfg = CONFIGS[args.config]
-    lib = rhp.lib()
-    lib.rhp_set_impl(args.impl)
+    if args.device == "gpu":
+        import torch
+        torch.cuda.set_device(local)
+        rhp.lib().rhp_set_impl(args.impl)
+    per_gpu = args.per_gpu or CONFIGS[args.config]["per_gpu"]
 
-    n_total = cfg["per_gpu"] * world
-    lo, hi = shard_range(n_total, rank, world)
-    buf, off = rhp.generate(cfg["gen"], hi - lo, cfg["seed"], lo=lo)
-    alg_bytes = rhp.header_bytes(cfg["gen"], hi - lo, cfg["seed"], lo=lo)
-    copies = [rhp.DeviceBatch(buf, off, cfg["maxh"], cfg["mode"]) for _ in range(max(1, args.copies))]
-    # the output buffers of copy 0 are shared so records stay in one place
-    for c in copies[1:]:
-        c.reqs, c.hdrs, c.http = copies[0].reqs, copies[0].hdrs, copies[0].http
-    stream = torch.cuda.current_stream()
-
-    def step(k):
-        copies[k % len(copies)].launch(stream)
-
-    for k in range(args.warmup):
-        step(k)
-    torch.cuda.synchronize()
-
-    # sanity: records of this shard are what the template says (cheap, host side)
-    res = copies[0].result()
-    ok_frac = float((res.reqs["ret"] > 0).mean()) if len(res.reqs) else 1.0
-
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for k in range(args.steps):
-        step(k)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    if world > 1:
-        torch.distributed.barrier()
-    kern_ms = ev0.elapsed_time(ev1) / args.steps   # avg launch duration on the launch stream
-
-    elapsed = wall
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-        tb = torch.tensor([float(alg_bytes)], dtype=torch.float64)
-        torch.distributed.all_reduce(tb)
-        total_alg = float(tb[0])
-    else:
-        total_alg = float(alg_bytes)
+    r = run_config(args.config, args, rank, world, per_gpu, args.steps, args.warmup, dist)
+    extra = {}
+    if world == 1 and args.extra == "auto" and args.config == "get256":
+        for key in ("zipf", "post"):
+            e = run_config(key, args, rank, world, args.per_gpu or CONFIGS[key]["per_gpu"], args.extra_steps,
+                           3, None)
+            extra[key] = {"workload": CONFIGS[key]["name"], "value": round(e["total_alg"] / (e["kern_ms"] * 1e-3)
+                                                                           / 2 ** 30, 2),
+                          "unit": "GiB/s", "steps": e["steps"], "ms_per_step": round(e["wall"] * 1e3 / e["steps"], 4),
+                          "ok_fraction": e["ok_frac"], "roofline": roofline(e, key)}
 
     if rank == 0:
-        ms_per_step = elapsed * 1e3 / args.steps
-        value = total_alg * args.steps / elapsed / 2 ** 30
-        per_launch = float(alg_bytes)
-        achieved = per_launch / (kern_ms * 1e-3) / 1e9
+        cfg = r["cfg"]
+        kernel = (rhp.lib().rhp_kernel_name().decode() if args.device == "gpu"
+                  else "rhp_emu_parse_batch (CPU emulation: harness test, not a measurement)")
         line = {
-            "metric": "GiB/s device-resident batched HTTP/1.1 request parse, 1/2/4/8 MI355X",
-            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "metric": METRIC,
+            "value": round(r["total_alg"] * r["steps"] / r["wall"] / 2 ** 30, 2), "unit": "GiB/s",
+            "n_gpus": world, "steps": r["steps"], "warmup": r["warmup"],
+            "ms_per_step": round(r["wall"] * 1e3 / r["steps"], 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": cfg["name"], "requests_per_gpu": hi - lo, "global_requests": n_total,
-                       "algorithmic_bytes_per_gpu": int(alg_bytes), "resident_copies": len(copies),
-                       "max_headers": cfg["maxh"], "parallelism": f"shard{world}", "ok_fraction": ok_frac,
-                       "kernel": lib.rhp_kernel_name().decode()},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profile(args.config),
-                         "kernel_ms": round(kern_ms, 4)},
+            "config": {"workload": cfg["name"], "requests_per_gpu": r["hi"] - r["lo"], "global_requests": r["n_total"],
+                       "algorithmic_bytes_per_gpu": int(r["alg_bytes"]), "resident_copies": args.copies,
+                       "max_headers": cfg["maxh"], "parallelism": f"shard{world}", "ok_fraction": r["ok_frac"],
+                       "kernel": kernel, "device": args.device},
+            "roofline": roofline(r, args.config),
         }
+        if extra:
+            line["extra_configs"] = extra
         if world == 1 and not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(cfg)
+            line["cpu_baseline"] = cpu_baseline([args.config] + [k for k in ("zipf", "post") if k in extra])
         print(json.dumps(line), flush=True)
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -17,8 +17,14 @@
  * from the request start (pointer - buf).  All buffers are device memory owned by
  * the caller; the call is asynchronous on `stream` (a hipStream_t).
  *
- * Records are compact (u16 offsets): a request longer than RHP_MAX_LEN bytes gets
- * ret = RHP_RET_TOOLONG and no other output.
+ * Requests of any length are parsed.  Records are compact (u16 offsets), so
+ * the one answer they cannot carry is a successful parse whose header section
+ * is longer than RHP_MAX_LEN bytes (phr ret > 65535): that request gets
+ * ret = RHP_RET_TOOLONG (and in RHP_MODE_HTTP result = RHP_RET_TOOLONG) and no
+ * other output; the caller parses it with a pointer-based parser
+ * (rhp_phr_parse_request / rhp_http_read_cpu, include/rhp_host.h).  -1, -2 and
+ * http results 0/-1 are exact at every length; body lengths and `consumed` are
+ * u64.
  */
 #ifndef RHP_H
 #define RHP_H
@@ -31,7 +37,7 @@ extern "C" {
 #endif
 
 #define RHP_PAD 256u            /* zero bytes required after the last request */
-#define RHP_MAX_LEN 65535u      /* longest request the u16 record format holds */
+#define RHP_MAX_LEN 65535u      /* longest header section (phr ret) the u16 records hold */
 #define RHP_MAX_HEADERS 64u     /* largest supported *num_headers capacity */
 #define RHP_RET_TOOLONG (-3)
 
@@ -43,7 +49,7 @@ enum rhp_mode {
 /* phr_parse_request result for one request (16 B).  For ret <= 0 only `ret`
  * is meaningful (the reference leaves the other outputs unspecified). */
 typedef struct rhp_req {
-  int32_t  ret;            /* >0 bytes consumed, -1 malformed, -2 partial, RHP_RET_TOOLONG */
+  int32_t  ret;            /* >0 bytes consumed, -1 malformed, -2 partial, RHP_RET_TOOLONG (ret > RHP_MAX_LEN) */
   uint16_t method_len;
   uint16_t path_off;
   uint16_t path_len;
@@ -66,7 +72,7 @@ typedef struct rhp_hdr {
 
 /* http_read_request result (24 B), RHP_MODE_HTTP only */
 typedef struct rhp_http {
-  int32_t  result;         /* 1 ready, 0 need more bytes / empty, -1 malformed */
+  int32_t  result;         /* 1 ready, 0 need more bytes / empty, -1 malformed, RHP_RET_TOOLONG */
   uint32_t body_kind;      /* 0: data_null(); 1: body = (req.ret, body_len) */
   uint64_t consumed;       /* bytes stream_consume() is given (mod 2^64, http.c:216) */
   uint64_t body_len;
@@ -86,15 +92,17 @@ typedef struct rhp_batch {
   rhp_req_t      *reqs;        /* device [n] */
   rhp_hdr_t      *hdrs;        /* device [n * max_headers] */
   rhp_http_t     *http;        /* device [n], RHP_MODE_HTTP */
-  uint32_t       *work;        /* device scratch, >= RHP_WORK_WORDS u32: zero it once before
-                                  the first call; every call leaves it zeroed again.  One
-                                  `work` per concurrently running call. */
+  uint32_t       *work;        /* reserved, may be NULL (device scratch of RHP_WORK_WORDS u32
+                                  for future kernels; the current ones keep their scheduling
+                                  state in LDS) */
 } rhp_batch_t;
 
 #define RHP_WORK_WORDS 64u
 
-/* Parse a batch on `stream` (hipStream_t).  Returns 0 on successful launch,
- * a negative errno-style code for bad arguments, or a positive hipError_t. */
+/* Parse a batch on `stream` (hipStream_t) of the calling thread's current
+ * device.  Returns 0 on successful launch, a negative errno-style code for bad
+ * arguments, or a positive hipError_t.  Thread-safe: one host thread per GPU
+ * may call it concurrently (per-device state is cached per device id). */
 int rhp_parse_batch(const rhp_batch_t *batch, void *stream);
 
 /* Which kernel implementation rhp_parse_batch uses (diagnostics / A-B tests). */
@@ -102,7 +110,7 @@ enum rhp_impl {
   RHP_IMPL_DFA = 0,    /* lane-per-request byte DFA with LDS tables (default) */
   RHP_IMPL_EXACT = 1   /* lane-per-request exact scalar path only (slow reference path) */
 };
-int rhp_set_impl(int impl);
+int rhp_set_impl(int impl);   /* per calling thread */
 
 /* Name of the kernel symbol the default implementation launches (for profiles). */
 const char *rhp_kernel_name(void);

@@ -7,8 +7,17 @@
  *                         "host" session parser use it
  *   rhp_emu_parse_batch   CPU emulation of the kernel's DFA algorithm, block for
  *                         block (tests only); stats[3] = fast ok, fast -1, exact
+ *   (both take an rhp_batch_t (include/rhp.h) whose pointers are host memory)
  *
- * Both take an rhp_batch_t (include/rhp.h) whose pointers are host memory.
+ *   rhp_phr_parse_request the same exact parser with phr_parse_request's own
+ *                         signature and outputs (pointers into buf, no length
+ *                         limit): a drop-in for
+ *                         /root/reference/src/picohttpparser/picohttpparser.h:51-52
+ *                         (last_len != 0 runs is_complete first, :197-223, :399-401)
+ *   rhp_http_read_cpu     http_read_request (/root/reference/src/reactor/http.c:177-234)
+ *                         over one buffer with pointer outputs: the reactor's
+ *                         http_read_request, and the server's path for requests
+ *                         whose records do not fit the batch format (RHP_RET_TOOLONG)
  */
 #ifndef RHP_HOST_H
 #define RHP_HOST_H
@@ -22,6 +31,38 @@ extern "C" {
 
 int rhp_cpu_parse_batch(const rhp_batch_t *batch);
 int rhp_emu_parse_batch(const rhp_batch_t *batch, uint64_t *stats);
+
+/* struct phr_header (picohttpparser.h:42-47): name == NULL for an obs-fold line */
+typedef struct rhp_phr_header {
+  const char *name;
+  size_t      name_len;
+  const char *value;
+  size_t      value_len;
+} rhp_phr_header_t;
+
+/* phr_parse_request: >0 bytes consumed, -1 malformed, -2 partial.  *num_headers
+ * is the capacity on input and the count on output.  As the reference, it may
+ * read bytes past buf + len while they are SP (picohttpparser.c:356-362). */
+int rhp_phr_parse_request(const char *buf, size_t len, const char **method, size_t *method_len, const char **path,
+                          size_t *path_len, int *minor_version, rhp_phr_header_t *headers, size_t *num_headers,
+                          size_t last_len);
+
+/* http_read_request's outputs for one buffer (http.c:177-234) */
+typedef struct rhp_http_req {
+  const char    *method;
+  size_t         method_len;
+  const char    *target;
+  size_t         target_len;
+  int            minor_version;
+  const uint8_t *body;       /* NULL: data_null() */
+  size_t         body_len;
+  uint64_t       consumed;   /* bytes stream_consume() is given (result 1) */
+} rhp_http_req_t;
+
+/* 1 ready, 0 need more bytes (or empty), -1 malformed.  *fields_count is the
+ * capacity on input, the count on output.  A chunked body is de-framed in place
+ * (http.c:155), so buf is written. */
+int rhp_http_read_cpu(uint8_t *buf, size_t len, rhp_http_req_t *req, rhp_phr_header_t *fields, size_t *fields_count);
 
 #ifdef __cplusplus
 }

@@ -53,7 +53,7 @@ class Batch(ctypes.Structure):
 # exported C-ABI symbols of librhp.so, as declared in include/rhp.h
 RHP_SYMBOLS = ("rhp_parse_batch", "rhp_set_impl", "rhp_kernel_name", "rhp_version", "rhp_write_responses")
 HOST_SYMBOLS = ("rhp_gen_size", "rhp_gen_fill", "rhp_gen_header_bytes", "rhp_splitmix64",
-                "rhp_emu_parse_batch", "rhp_cpu_parse_batch")
+                "rhp_emu_parse_batch", "rhp_cpu_parse_batch", "rhp_phr_parse_request", "rhp_http_read_cpu")
 
 _rhp = None
 _host = None
@@ -106,7 +106,62 @@ def host() -> ctypes.CDLL:
         _host.rhp_emu_parse_batch.restype = ctypes.c_int
         _host.rhp_cpu_parse_batch.argtypes = [ctypes.POINTER(Batch)]
         _host.rhp_cpu_parse_batch.restype = ctypes.c_int
+        sz, vp = ctypes.c_size_t, ctypes.c_void_p
+        P = ctypes.POINTER
+        _host.rhp_phr_parse_request.argtypes = [vp, sz, P(vp), P(sz), P(vp), P(sz), P(ctypes.c_int),
+                                                P(PhrHeader), P(sz), sz]
+        _host.rhp_phr_parse_request.restype = ctypes.c_int
+        _host.rhp_http_read_cpu.argtypes = [vp, sz, P(HttpReq), P(PhrHeader), P(sz)]
+        _host.rhp_http_read_cpu.restype = ctypes.c_int
     return _host
+
+
+class PhrHeader(ctypes.Structure):
+    """struct phr_header (picohttpparser.h:42-47) = rhp_phr_header_t (include/rhp_host.h)."""
+    _fields_ = [("name", ctypes.c_void_p), ("name_len", ctypes.c_size_t), ("value", ctypes.c_void_p),
+                ("value_len", ctypes.c_size_t)]
+
+
+class HttpReq(ctypes.Structure):
+    """rhp_http_req_t (include/rhp_host.h)."""
+    _fields_ = [("method", ctypes.c_void_p), ("method_len", ctypes.c_size_t), ("target", ctypes.c_void_p),
+                ("target_len", ctypes.c_size_t), ("minor_version", ctypes.c_int), ("body", ctypes.c_void_p),
+                ("body_len", ctypes.c_size_t), ("consumed", ctypes.c_uint64)]
+
+
+def phr_parse_request_cpu(buf: np.ndarray, start: int, length: int, max_headers: int, last_len: int = 0):
+    """rhp_phr_parse_request (the host drop-in for phr_parse_request) on bytes
+    buf[start:start+length] (buf may be read past the end, as the reference does).
+    Returns (ret, minor, method(off,len), path(off,len), [(name_off|-1, name_len,
+    value_off, value_len)]) with offsets from `start`."""
+    h = host()
+    hdrs = (PhrHeader * max(max_headers, 1))()
+    m, pth = ctypes.c_void_p(), ctypes.c_void_p()
+    ml, pl, nh = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t(max_headers)
+    minor = ctypes.c_int()
+    base = buf.ctypes.data + start
+    ret = h.rhp_phr_parse_request(base, length, ctypes.byref(m), ctypes.byref(ml), ctypes.byref(pth),
+                                  ctypes.byref(pl), ctypes.byref(minor), hdrs, ctypes.byref(nh), last_len)
+    if ret <= 0:
+        return ret, -1, (0, 0), (0, 0), []
+    rel = lambda p: (p or 0) - base
+    hs = [(rel(x.name) if x.name else -1, x.name_len, rel(x.value), x.value_len) for x in hdrs[: nh.value]]
+    return ret, minor.value, (rel(m.value), ml.value), (rel(pth.value), pl.value), hs
+
+
+def http_read_cpu(buf: np.ndarray, start: int, length: int, max_headers: int = 16):
+    """rhp_http_read_cpu (http_read_request with pointer outputs) on buf[start:start+length]
+    (written in place for chunked bodies).  Returns (result, consumed, body(off,len) | None)."""
+    h = host()
+    hdrs = (PhrHeader * max(max_headers, 1))()
+    r = HttpReq()
+    nh = ctypes.c_size_t(max_headers)
+    base = buf.ctypes.data + start
+    res = h.rhp_http_read_cpu(base, length, ctypes.byref(r), hdrs, ctypes.byref(nh))
+    if res != 1:
+        return res, 0, None
+    body = (r.body - base, r.body_len) if r.body else None
+    return res, int(r.consumed), body
 
 
 def _ptr(a: np.ndarray) -> int:

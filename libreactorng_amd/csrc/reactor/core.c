@@ -84,6 +84,9 @@ size_t buffer_capacity(const buffer_t *b) { return b->capacity; }
 void *buffer_base(const buffer_t *b) { return data_base(b->data); }
 void *buffer_end(const buffer_t *b) { return data_end(b->data); }
 
+/* power-of-two capacity (buffer.c:6-17, 56-64), plus RHP_PAD zero bytes past
+ * it that nothing writes: the parser's reads past the input (the SP skip of
+ * picohttpparser.c:356-362) stay inside the allocation and stop there */
 void buffer_reserve(buffer_t *b, size_t capacity)
 {
   if (capacity <= b->capacity)
@@ -91,9 +94,10 @@ void buffer_reserve(buffer_t *b, size_t capacity)
   size_t c = b->capacity ? b->capacity : 64;
   while (c < capacity)
     c *= 2;
-  void *p = realloc(data_base(b->data), c);
+  char *p = realloc(data_base(b->data), c + RHP_PAD);
   if (!p)
     abort();
+  memset(p + c, 0, RHP_PAD);
   b->data.iov.iov_base = p;
   b->capacity = c;
 }

@@ -4,9 +4,10 @@
  *
  *   http_read_request    one request from a stream (http.c:177-234): the same
  *                        contract, answered by the product's exact parser on
- *                        the host (rhp_cpu_parse_batch, a batch of one).  The
- *                        server does not call it: sessions are parsed in
- *                        batches on the GPU (server.c).
+ *                        the host with pointer outputs (rhp_http_read_cpu, no
+ *                        length limit).  The server parses sessions in batches
+ *                        on the GPU (server.c) and uses it only for requests
+ *                        the batch records cannot hold (RHP_RET_TOOLONG).
  *   http_write_response  the response serializer (http.c:236-297): status
  *                        line, Server / Date / Content-Type / Content-Length,
  *                        the caller's fields, blank line, body.
@@ -52,22 +53,22 @@ int http_read_request(stream_t *stream, string_t *method, string_t *target, data
                       size_t *fields_count)
 {
   data_t input = stream_read(stream);
-  if (data_empty(input))
-    return 0;
-  rhp_hdr_t h[RHP_MAX_HEADERS];
-  rhp_req_t r;
-  rhp_http_t x;
-  uint64_t offsets[2] = {0, data_size(input)};
-  uint32_t maxh = *fields_count < RHP_MAX_HEADERS ? (uint32_t) *fields_count : RHP_MAX_HEADERS;
-  rhp_batch_t b = {
-    .bytes = data_base(input), .bytes_rw = data_base(input), .offsets = offsets,
-    .bytes_size = data_size(input) + RHP_PAD, .n = 1, .max_headers = maxh, .mode = RHP_MODE_HTTP,
-    .reqs = &r, .hdrs = h, .http = &x};
-  (void) rhp_cpu_parse_batch(&b);
-  if (x.result != 1)
-    return x.result;
-  reactor_http_fill(data_base(input), &r, h, &x, method, target, body, fields, fields_count);
-  stream_consume(stream, x.consumed);
+  rhp_http_req_t r;
+  rhp_phr_header_t h[RHP_MAX_HEADERS];
+  size_t n = *fields_count < RHP_MAX_HEADERS ? *fields_count : RHP_MAX_HEADERS;
+  int result = rhp_http_read_cpu(data_base(input), data_size(input), &r, h, &n);
+  if (result != 1)
+    return result;
+  *method = data(r.method, r.method_len);
+  *target = data(r.target, r.target_len);
+  for (size_t k = 0; k < n; k++)
+  {
+    fields[k].name = h[k].name ? data(h[k].name, h[k].name_len) : data_null();
+    fields[k].value = data(h[k].value, h[k].value_len);
+  }
+  *fields_count = n;
+  *body = r.body ? data(r.body, r.body_len) : data_null();
+  stream_consume(stream, r.consumed);
   return 1;
 }
 

@@ -228,22 +228,38 @@ static bool server_session_dispatch(server_session_t *s, const piece_t *pc, size
       more = true;
       break;
     }
-    if (x->result == -1)
+    int result = x->result;
+    size_t consumed = 0;
+    if (result == RHP_RET_TOOLONG)
+    {
+      /* a header section the batch records cannot hold (> RHP_MAX_LEN): the
+       * pointer-based host parser answers for this request */
+      s->request.fields_count = REACTOR_BATCH_HEADERS;
+      const size_t before = data_size(in);
+      result = http_read_request(&s->stream, &s->request.method, &s->request.target, &s->request.body,
+                                 s->request.fields, &s->request.fields_count);
+      consumed = before - data_size(stream_read(&s->stream));
+    }
+    if (result == -1)
     {
       server_session_close(s);
       return true;
     }
-    if (x->result == 0)
+    if (result == 0)
       break;
-    const uint64_t off = reactor_batch_offsets()[p->index];
-    uint8_t *base = data_base(in);
-    if (x->body_kind && x->consumed != (uint64_t) res->reqs[p->index].ret + x->body_len)
-      memcpy(base, res->bytes + off, x->consumed);   /* chunked body, de-framed in place */
-    reactor_http_fill(base, &res->reqs[p->index], res->hdrs + (size_t) p->index * REACTOR_BATCH_HEADERS, x,
-                      &s->request.method, &s->request.target, &s->request.body, s->request.fields,
-                      &s->request.fields_count);
-    stream_consume(&s->stream, x->consumed);
-    at += x->consumed;
+    if (x->result != RHP_RET_TOOLONG)
+    {
+      const uint64_t off = reactor_batch_offsets()[p->index];
+      uint8_t *base = data_base(in);
+      if (x->body_kind && x->consumed != (uint64_t) res->reqs[p->index].ret + x->body_len)
+        memcpy(base, res->bytes + off, x->consumed);   /* chunked body, de-framed in place */
+      reactor_http_fill(base, &res->reqs[p->index], res->hdrs + (size_t) p->index * REACTOR_BATCH_HEADERS, x,
+                        &s->request.method, &s->request.target, &s->request.body, s->request.fields,
+                        &s->request.fields_count);
+      consumed = x->consumed;
+      stream_consume(&s->stream, consumed);
+    }
+    at += consumed;
     k++;
     s->flags &= ~SERVER_SESSION_READY;
     s->flags |= SERVER_SESSION_PROCESSING;

@@ -37,8 +37,9 @@
  * empty method, more than one SP between request-line fields, versions other
  * than HTTP/1.0 and HTTP/1.1, bare-LF line ends, anything but exactly one SP
  * after a header colon (":v", ":\tv", ":  v", ":\r\n"), OWS before a CR
- * (value trimming), obs-fold continuation lines, requests longer than
- * kFastMaxLen.
+ * (value trimming), obs-fold continuation lines.  A header section longer
+ * than the u16 records hold (ret > RHP_MAX_LEN) is also handed to the exact
+ * path, which answers RHP_RET_TOOLONG; requests of any length are walked.
  */
 #ifndef RHP_DFA_H
 #define RHP_DFA_H
@@ -76,10 +77,6 @@ enum State : uint32_t {
   S_COLON_E,     /* CO */
   S_LINE_E,      /* EOL */
   S_COUNT
-};
-
-enum : uint32_t {
-  kFastMaxLen = 65535 - 256    /* longer requests take the exact path (u16 positions) */
 };
 
 /* u8 index of a state: plain states even, event states odd */
@@ -335,11 +332,11 @@ constexpr Table2 make_table2()
 }
 
 /*
- * Event decoder state of one request.  hist holds the last four event positions
- * as u16: h01 = e0 | e1 << 16, h23 = e2 | e3 << 16 (e0 newest).
+ * Event decoder state of one request (the emulator's form of the kernel's
+ * anchor decode).  e[0..3] hold the last four event positions, e[0] newest.
  */
 struct Dec {
-  uint32_t h01, h23;
+  uint32_t e[4];
   uint32_t k;       /* events consumed: 0..2 request line, then 3,4 = CO, EOL */
   uint32_t nh;      /* header lines completed */
   uint32_t rl01;    /* method_len | path_off << 16 */
@@ -349,7 +346,7 @@ struct Dec {
 
 RHP_DHD inline void dec_reset(Dec &d)
 {
-  d.h01 = d.h23 = 0;
+  d.e[0] = d.e[1] = d.e[2] = d.e[3] = 0;
   d.k = 0;
   d.nh = 0;
   d.rl01 = d.rl23 = 0;
@@ -361,34 +358,37 @@ RHP_DHD inline void dec_reset(Dec &d)
  * record completed that is to be stored at index d.nh - 1 (< max_headers):
  * (lo, hi) = (name_off | name_len << 16, value_off | value_len << 16).
  * Sets d.ovf when the reference's max_headers check fires (picohttpparser.c:
- * 281-284: a new line starts while num_headers == max_headers).
+ * 281-284: a new line starts while num_headers == max_headers).  Records are
+ * u16: they are only used when the request ends below RHP_MAX_LEN.
  */
 RHP_DHD inline bool dec_event(Dec &d, uint32_t p, uint32_t maxh, uint32_t &lo, uint32_t &hi)
 {
-  d.h23 = (d.h23 << 16) | (d.h01 >> 16);
-  d.h01 = (d.h01 << 16) | p;
+  d.e[3] = d.e[2];
+  d.e[2] = d.e[1];
+  d.e[1] = d.e[0];
+  d.e[0] = p;
   if (d.k < 2) {
     d.k++;
     return false;
   }
   if (d.k == 2) {   /* RL: history = RL, PE, ME */
-    const uint32_t pe = d.h01 >> 16, me = d.h23 & 0xffffu;
+    const uint32_t pe = d.e[1], me = d.e[2];
     const uint32_t minor = p - pe - 9u;   /* 0 (event at the CR) or 1 (at the LF) */
-    d.rl01 = me | ((me + 1u) << 16);
-    d.rl23 = (pe - me - 1u) | (minor << 16);
-    d.h01 = (d.h01 & 0xffff0000u) | (pe + 10u);   /* e0 := the LF that ends the request line */
+    d.rl01 = (me & 0xffffu) | ((me + 1u) << 16);
+    d.rl23 = ((pe - me - 1u) & 0xffffu) | (minor << 16);
+    d.e[0] = pe + 10u;   /* e0 := the LF that ends the request line */
     d.k = 3;
     return false;
   }
   if (d.k == 3) {   /* CO: history = CO, prevLF, ... */
-    if (d.nh == maxh && d.ovf == 0) d.ovf = 1u + (d.h01 >> 16) + 1u;
+    if (d.nh == maxh && d.ovf == 0) d.ovf = 1u + d.e[1] + 1u;
     d.k = 4;
     return false;
   }
   /* EOL: history = LF, CO, prevLF */
-  const uint32_t lf = p, co = d.h01 >> 16, prev = d.h23 & 0xffffu;
-  lo = (prev + 1u) | ((co - prev - 1u) << 16);
-  hi = (co + 2u) | ((lf - co - 3u) << 16);
+  const uint32_t lf = p, co = d.e[1], prev = d.e[2];
+  lo = ((prev + 1u) & 0xffffu) | ((co - prev - 1u) << 16);
+  hi = ((co + 2u) & 0xffffu) | ((lf - co - 3u) << 16);
   d.k = 3;
   d.nh++;
   return d.nh <= maxh;

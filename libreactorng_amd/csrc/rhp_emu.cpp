@@ -36,15 +36,6 @@ void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
   rhp_req_t r;
   r.flags = RHP_F_EXACT;
   rhp_hdr_t *h = b->hdrs + (uint64_t) i * b->max_headers;
-  if (len > RHP_MAX_LEN) {
-    memset(&r, 0, sizeof r);
-    r.ret = RHP_RET_TOOLONG;
-    r.minor_version = -1;
-    r.flags = RHP_F_EXACT;
-    b->reqs[i] = r;
-    if (b->mode == RHP_MODE_HTTP) memset(&b->http[i], 0, sizeof b->http[i]);
-    return;
-  }
   if (b->mode == RHP_MODE_HTTP) scalar_http(b->bytes_rw + off, len, b->max_headers, &r, h, &b->http[i]);
   else scalar_phr(b->bytes + off, len, b->max_headers, &r, h);
   b->reqs[i] = r;
@@ -65,7 +56,6 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
     const uint8_t *win = b->bytes + (off - mis);
     int32_t pos = -(int32_t) mis;
     uint32_t s0 = mis == 0 ? S_METHOD0 : mis == 1 ? S_SKIP1 : mis == 2 ? S_SKIP2 : S_SKIP3;
-    if (len > kFastMaxLen) s0 = S_SLOW;
     uint32_t st = idx2(s0, 0);
     Dec d;
     dec_reset(d);
@@ -114,7 +104,7 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
       const bool ovf = d.ovf != 0;
       if (!(ovf || slow || term_ev || pos >= (int32_t) len)) continue;
       /* ---- finalize (same decisions as the kernel) ---- */
-      const bool ok = !ovf && is_done2(st) && term_pos < len;
+      const bool ok = !ovf && is_done2(st) && term_pos < len && term_pos < RHP_MAX_LEN;
       const bool bad = ovf ? d.ovf - 1u < len : (is_err2(st) && term_pos < len);
       if (ok) {
         st_count.fast_ok++;
@@ -160,4 +150,88 @@ extern "C" int rhp_cpu_parse_batch(const rhp_batch_t *b)
 {
   for (uint32_t i = 0; i < b->n; i++) emu_exact(b, i, b->offsets[i], b->offsets[i + 1] - b->offsets[i]);
   return 0;
+}
+
+/* ---- the pointer-based host parser: phr_parse_request's own outputs ---- */
+
+namespace {
+
+/* rhp_scalar.h output policy writing phr_parse_request's outputs (pointers
+ * into buf, size_t lengths): no length limit */
+struct OutPhr {
+  const uint8_t *base;
+  const char **method;
+  size_t *method_len;
+  const char **path;
+  size_t *path_len;
+  int *minor_version;
+  rhp_phr_header_t *h;
+  size_t *num_headers;
+  void begin()
+  {
+    *method = nullptr; *method_len = 0; *path = nullptr; *path_len = 0;   /* picohttpparser.c:390-395 */
+    *minor_version = -1; *num_headers = 0;
+  }
+  int fail(int code) { return code; }
+  void header(uint32_t n, bool fold, uint64_t name, uint64_t name_len, uint64_t vs, uint64_t vlen)
+  {
+    h[n].name = fold ? nullptr : (const char *) base + name;
+    h[n].name_len = (size_t) name_len;
+    h[n].value = (const char *) base + vs;
+    h[n].value_len = (size_t) vlen;
+  }
+  int done(uint64_t p, const uint64_t (&tok)[2][2], int minor, uint32_t n)
+  {
+    *method = (const char *) base + tok[0][0];
+    *method_len = (size_t) (tok[0][1] - tok[0][0]);
+    *path = (const char *) base + tok[1][0];
+    *path_len = (size_t) (tok[1][1] - tok[1][0]);
+    *minor_version = minor;
+    *num_headers = n;
+    return (int) p;
+  }
+};
+
+/* rhp_scalar.h header view over phr_header records */
+struct HdrsPhr {
+  const rhp_phr_header_t *h;
+  bool null(uint32_t i) const { return h[i].name == nullptr; }
+  const uint8_t *name(uint32_t i) const { return (const uint8_t *) h[i].name; }
+  uint64_t name_len(uint32_t i) const { return h[i].name_len; }
+  const uint8_t *value(uint32_t i) const { return (const uint8_t *) h[i].value; }
+  uint64_t value_len(uint32_t i) const { return h[i].value_len; }
+};
+
+}  // namespace
+
+extern "C" int rhp_phr_parse_request(const char *buf, size_t len, const char **method, size_t *method_len,
+                                     const char **path, size_t *path_len, int *minor_version,
+                                     rhp_phr_header_t *headers, size_t *num_headers, size_t last_len)
+{
+  const uint8_t *b = (const uint8_t *) buf;
+  const size_t max = *num_headers;
+  OutPhr o{b, method, method_len, path, path_len, minor_version, headers, num_headers};
+  if (last_len != 0) {   /* picohttpparser.c:399-401 */
+    o.begin();
+    const int r = is_complete(b, len, last_len);
+    if (r != 0) return r;
+  }
+  PlainBytes B{b};
+  return scalar_phr_t(B, len, (uint32_t) (max < 0xffffffffu ? max : 0xffffffffu), o);
+}
+
+extern "C" int rhp_http_read_cpu(uint8_t *buf, size_t len, rhp_http_req_t *req, rhp_phr_header_t *fields,
+                                 size_t *fields_count)
+{
+  if (len == 0) return 0;                               /* http.c:184-186 */
+  const int n = rhp_phr_parse_request((const char *) buf, len, &req->method, &req->method_len, &req->target,
+                                      &req->target_len, &req->minor_version, fields, fields_count, 0);
+  if (n <= 0) return n == kBad ? -1 : 0;                /* http.c:194-195 */
+  const bool get = req->method_len == 3 && memcmp(req->method, "GET", 3) == 0;
+  rhp_http_t x;
+  http_frame_t(buf, len, n, get, HdrsPhr{fields}, (uint32_t) *fields_count, &x);
+  req->body = x.body_kind ? buf + n : nullptr;
+  req->body_len = x.body_kind ? (size_t) x.body_len : 0;
+  req->consumed = x.consumed;
+  return x.result;
 }

@@ -32,6 +32,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 #include <stdlib.h>
 #include <string.h>
 
@@ -195,17 +196,6 @@ __device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64
   rhp_req_t r;
   r.flags = RHP_F_EXACT;
   rhp_hdr_t *h = p.hdrs + (uint64_t) i * p.max_headers;
-  if (len > RHP_MAX_LEN) {
-    r.ret = RHP_RET_TOOLONG;
-    r.method_len = r.path_off = r.path_len = 0;
-    r.method_off = 0; r.minor_version = -1; r.num_headers = 0;
-    p.reqs[i] = r;
-    if (p.mode == RHP_MODE_HTTP) {
-      rhp_http_t x = {0, 0, 0, 0};
-      p.http[i] = x;
-    }
-    return;
-  }
   if (p.mode == RHP_MODE_HTTP) {
     rhp_http_t x;
     LineBytes B{p.bytes_rw + off, ~0ull, {0, 0, 0, 0}};
@@ -694,7 +684,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const bool ovfl = ovf_at != 0;
     const bool fin = ovfl || slow || term_ev || (uint32_t) pos >= cur_len;
     if (!fin) return;
-    const bool ok = !ovfl && t_done(e) && term_pos < cur_len;
+    /* a header section the u16 records cannot hold (ret > RHP_MAX_LEN) is left
+     * to the exact path, which answers RHP_RET_TOOLONG */
+    const bool ok = !ovfl && t_done(e) && term_pos < cur_len && term_pos < RHP_MAX_LEN;
     const bool bad = ovfl ? ovf_at - 1u < cur_len : (t_err(e) && term_pos < cur_len);
     rhp_req_t r = {};
     r.minor_version = -1;
@@ -1035,7 +1027,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       has = true;
       const uint32_t mis = (uint32_t) p_o0 & 3u;
       uint32_t s0 = mis == 0 ? S_METHOD0 : mis == 1 ? S_SKIP1 : mis == 2 ? S_SKIP2 : S_SKIP3;
-      if (cur_len > kFastMaxLen) s0 = S_SLOW;
       st = start_index(s0);
       pos = -(int32_t) mis;
       kn = A = B = ovf = rl = 0;
@@ -1167,25 +1158,43 @@ __global__ __launch_bounds__(256) void rhp_exact_kernel(Params p)
 /* ------------------------------- host C-ABI ------------------------------- */
 
 namespace {
-int g_impl = RHP_IMPL_DFA;
-int g_cus = 0;
+/* Host state is per device and safe for one host thread per GPU (SURVEY.md
+ * §8e): the CU count and the kernel's LDS attribute are cached per device id,
+ * the implementation choice (rhp_set_impl, diagnostics) is per thread. */
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_cus[kMaxDevices];
+std::atomic<uint32_t> g_attr[kMaxDevices];   /* bit w: the LDS attribute of rhp_dfa_kernel<w> is set */
+thread_local int t_impl = RHP_IMPL_DFA;
+
+int device_cus(int dev, int *cus)
+{
+  int c = g_cus[dev].load(std::memory_order_relaxed);
+  if (c == 0) {
+    hipError_t e = hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return (int) e;
+    g_cus[dev].store(c, std::memory_order_relaxed);
+  }
+  *cus = c;
+  return 0;
+}
 
 template <int WAVES>
-int launch_dfa(const Params &prm, hipStream_t s)
+int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
 {
   const size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes;
-  static bool attr_set = false;
-  if (!attr_set) {
+  const uint32_t bit = 1u << (WAVES / 4);
+  if (!(g_attr[dev].load(std::memory_order_acquire) & bit)) {
+    /* idempotent: two threads of one device may both set it */
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds_bytes);
     if (e != hipSuccess) return (int) e;
-    attr_set = true;
+    g_attr[dev].fetch_or(bit, std::memory_order_release);
   }
   int per_cu = 0;
   hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rhp_dfa_kernel<WAVES>, WAVES * 64, lds_bytes);
   if (e != hipSuccess) return (int) e;
   if (per_cu < 1) per_cu = 1;
-  uint32_t grid = (uint32_t) (g_cus * per_cu);
+  uint32_t grid = (uint32_t) (cus * per_cu);
   uint32_t need = (prm.n + 64 * WAVES - 1) / (64 * WAVES);
   if (grid > need) grid = need > 0 ? need : 1;
   /* each workgroup owns a contiguous n/grid share of the requests */
@@ -1195,15 +1204,13 @@ int launch_dfa(const Params &prm, hipStream_t s)
   return (int) hipGetLastError();
 }
 
-int g_waves = -1;   /* RHP_WAVES (experiments): waves per workgroup */
-
-int dfa_waves()
+int dfa_waves()   /* RHP_WAVES (experiments): waves per workgroup */
 {
-  if (g_waves < 0) {
+  static const int w = [] {
     const char *e = getenv("RHP_WAVES");
-    g_waves = e ? atoi(e) : 16;
-  }
-  return g_waves;
+    return e ? atoi(e) : 16;
+  }();
+  return w;
 }
 }  // namespace
 
@@ -1224,12 +1231,12 @@ int rhp_debug_stamps_end(unsigned long long *host)
 }
 #endif
 
-const char *rhp_kernel_name(void) { return g_impl == RHP_IMPL_EXACT ? "rhp_exact_kernel" : "rhp_dfa_kernel"; }
+const char *rhp_kernel_name(void) { return t_impl == RHP_IMPL_EXACT ? "rhp_exact_kernel" : "rhp_dfa_kernel"; }
 
 int rhp_set_impl(int impl)
 {
   if (impl != RHP_IMPL_DFA && impl != RHP_IMPL_EXACT) return -22;
-  g_impl = impl;
+  t_impl = impl;
   return 0;
 }
 
@@ -1237,18 +1244,20 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
 {
   if (!b) return -22;
   if (b->n == 0) return 0;                       /* nothing to parse, nothing touched */
-  if (!b->bytes || !b->offsets || !b->reqs || !b->work) return -22;
+  if (!b->bytes || !b->offsets || !b->reqs) return -22;
   if (((uintptr_t) b->bytes & 15u) != 0) return -22;   /* windows and exact-path lines are aligned loads */
   if (b->max_headers > RHP_MAX_HEADERS) return -22;
   if (b->max_headers > 0 && !b->hdrs) return -22;
   if (b->mode == RHP_MODE_HTTP && (!b->http || !b->bytes_rw)) return -22;
   if (b->mode != RHP_MODE_PHR && b->mode != RHP_MODE_HTTP) return -22;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (g_cus == 0) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+  int dev = 0, cus = 0;
+  {
+    hipError_t e = hipGetDevice(&dev);   /* the calling thread's current device */
     if (e != hipSuccess) return (int) e;
+    if (dev < 0 || dev >= kMaxDevices) return -22;
+    const int rc = device_cus(dev, &cus);
+    if (rc != 0) return rc;
   }
 
   Params prm;
@@ -1266,17 +1275,17 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
 
   /* the DFA kernel addresses windows with u32 offsets from its range start;
    * batches of 4 GiB or more take the exact kernel */
-  if (g_impl == RHP_IMPL_EXACT || b->bytes_size >= 0xFFFF0000ull) {
+  if (t_impl == RHP_IMPL_EXACT || b->bytes_size >= 0xFFFF0000ull) {
     uint32_t grid = (b->n + 255) / 256;
-    if (grid > (uint32_t) g_cus * 8) grid = (uint32_t) g_cus * 8;
+    if (grid > (uint32_t) cus * 8) grid = (uint32_t) cus * 8;
     hipLaunchKernelGGL(rhp_exact_kernel, dim3(grid), dim3(256), 0, s, prm);
     return (int) hipGetLastError();
   }
   switch (dfa_waves()) {
-  case 4: return launch_dfa<4>(prm, s);
-  case 8: return launch_dfa<8>(prm, s);
-  case 12: return launch_dfa<12>(prm, s);
-  default: return launch_dfa<16>(prm, s);
+  case 4: return launch_dfa<4>(prm, s, dev, cus);
+  case 8: return launch_dfa<8>(prm, s, dev, cus);
+  case 12: return launch_dfa<12>(prm, s, dev, cus);
+  default: return launch_dfa<16>(prm, s, dev, cus);
   }
 }
 

@@ -50,15 +50,52 @@ struct PlainBytes {
   RHP_HDM uint32_t operator()(uint64_t p) const { return b[p]; }
 };
 
-/* Parse one request.  b may be read beyond len (batch contract).  Headers are
- * written to h[0..max).  Returns the phr status; fills r. */
-template <class Bytes>
-RHP_HD int scalar_phr_t(Bytes &B, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h)
+/* Where the exact parser puts its answer (the same parse, two encodings).
+ *   OutRec  the batch records of rhp.h: offsets from the request start as u16.
+ *           A header section longer than RHP_MAX_LEN (phr ret > 65535) cannot
+ *           be encoded and gives RHP_RET_TOOLONG; every other answer (-1, -2,
+ *           or a ret that fits) is the reference's, whatever the buffer length.
+ *   OutPhr  (host, rhp_emu.cpp) phr_parse_request's own outputs: pointers into
+ *           the buffer and size_t lengths, no limit (picohttpparser.h:51-52). */
+struct OutRec {
+  rhp_req_t *r;
+  rhp_hdr_t *h;
+  RHP_HDM void begin()
+  {
+    r->method_off = 0; r->method_len = 0; r->path_off = 0; r->path_len = 0;
+    r->minor_version = -1; r->num_headers = 0;
+  }
+  RHP_HDM int fail(int code) { r->ret = code; return code; }
+  RHP_HDM void header(uint32_t n, bool fold, uint64_t name, uint64_t name_len, uint64_t vs, uint64_t vlen)
+  {
+    h[n].name_off = fold ? (uint16_t) RHP_NAME_NULL : (uint16_t) name;
+    h[n].name_len = (uint16_t) name_len;
+    h[n].value_off = (uint16_t) vs;
+    h[n].value_len = (uint16_t) vlen;
+  }
+  RHP_HDM int done(uint64_t p, const uint64_t (&tok)[2][2], int minor, uint32_t n)
+  {
+    if (p > RHP_MAX_LEN) return fail(RHP_RET_TOOLONG);   /* u16 records cannot hold it */
+    r->method_off = (uint8_t) tok[0][0];
+    r->method_len = (uint16_t) (tok[0][1] - tok[0][0]);
+    r->path_off = (uint16_t) tok[1][0];
+    r->path_len = (uint16_t) (tok[1][1] - tok[1][0]);
+    r->minor_version = (int8_t) minor;
+    r->num_headers = (uint16_t) n;
+    r->ret = (int32_t) p;
+    return r->ret;
+  }
+};
+
+/* Parse one request (parse_request, picohttpparser.c:341-381).  b may be read
+ * beyond len (batch contract).  Headers go to out.header(0 .. max-1).  Returns
+ * the phr status (or RHP_RET_TOOLONG from OutRec). */
+template <class Bytes, class Out>
+RHP_HD int scalar_phr_t(Bytes &B, uint64_t len, uint32_t max, Out &out)
 {
   uint64_t p = 0;
-  r->method_off = 0; r->method_len = 0; r->path_off = 0; r->path_len = 0;
-  r->minor_version = -1; r->num_headers = 0;
-#define RHP_FAIL(code) do { r->ret = (code); return (code); } while (0)
+  out.begin();
+#define RHP_FAIL(code) do { return out.fail(code); } while (0)
 #define RHP_EOF() do { if (p == len) RHP_FAIL(kPartial); } while (0)
 #define RHP_CRLF() do { ++p; RHP_EOF(); if (B(p++) != '\n') RHP_FAIL(kBad); } while (0)
   RHP_EOF();
@@ -126,23 +163,20 @@ RHP_HD int scalar_phr_t(Bytes &B, uint64_t len, uint32_t max, rhp_req_t *r, rhp_
     else if (c == '\n') ++p;
     else RHP_FAIL(kBad);
     while (ve > vs && is_ows(B(ve - 1))) --ve;
-    h[n].name_off = fold ? (uint16_t) RHP_NAME_NULL : (uint16_t) name;
-    h[n].name_len = (uint16_t) name_len;
-    h[n].value_off = (uint16_t) vs;
-    h[n].value_len = (uint16_t) (ve - vs);
+    out.header(n, fold, name, name_len, vs, ve - vs);
     ++n;
   }
 #undef RHP_CRLF
 #undef RHP_EOF
 #undef RHP_FAIL
-  r->method_off = (uint8_t) tok[0][0];
-  r->method_len = (uint16_t) (tok[0][1] - tok[0][0]);
-  r->path_off = (uint16_t) tok[1][0];
-  r->path_len = (uint16_t) (tok[1][1] - tok[1][0]);
-  r->minor_version = (int8_t) minor;
-  r->num_headers = (uint16_t) n;
-  r->ret = (int32_t) p;
-  return r->ret;
+  return out.done(p, tok, minor, n);
+}
+
+template <class Bytes>
+RHP_HD int scalar_phr_t(Bytes &B, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h)
+{
+  OutRec o{r, h};
+  return scalar_phr_t(B, len, max, o);
 }
 
 RHP_HD int scalar_phr(const uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h)
@@ -151,18 +185,57 @@ RHP_HD int scalar_phr(const uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r
   return scalar_phr_t(B, len, max, r, h);
 }
 
+/* is_complete (picohttpparser.c:197-223), the slowloris pre-check that
+ * phr_parse_request runs first when last_len != 0 (:399-401): 0 when an empty
+ * line ends the bytes seen (scanning from last_len - 3), else -2 / -1. */
+RHP_HD int is_complete(const uint8_t *b, uint64_t len, uint64_t last_len)
+{
+  uint64_t p = last_len < 3 ? 0 : last_len - 3;
+  int ret_cnt = 0;
+  for (;;) {
+    if (p == len) return kPartial;
+    if (b[p] == '\r') {
+      ++p;
+      if (p == len) return kPartial;
+      if (b[p++] != '\n') return kBad;
+      ++ret_cnt;
+    } else if (b[p] == '\n') {
+      ++p;
+      ++ret_cnt;
+    } else {
+      ++p;
+      ret_cnt = 0;
+    }
+    if (ret_cnt == 2) return 0;
+  }
+}
+
 /* ---- http_read_request framing (http.c:177-234) over a parsed request ---- */
 
 RHP_HD uint32_t upper(uint32_t c) { return (c - 'a' < 26u) ? c - 32u : c; }
 
+/* Header views for the framing: HdrsRec reads the batch records (offsets from
+ * the request start b), a host view (rhp_emu.cpp) reads phr_header pointers. */
+struct HdrsRec {
+  const uint8_t *b;
+  const rhp_hdr_t *h;
+  RHP_HDM bool null(uint32_t i) const { return h[i].name_off == RHP_NAME_NULL; }
+  RHP_HDM const uint8_t *name(uint32_t i) const { return b + h[i].name_off; }
+  RHP_HDM uint64_t name_len(uint32_t i) const { return h[i].name_len; }
+  RHP_HDM const uint8_t *value(uint32_t i) const { return b + h[i].value_off; }
+  RHP_HDM uint64_t value_len(uint32_t i) const { return h[i].value_len; }
+};
+
 /* Case-insensitive name compare.  All n bytes are read before any is tested
  * (no early exit), so on the GPU replay path they are independent loads: one
  * memory round trip instead of n dependent ones. */
-RHP_HD bool name_eq(const uint8_t *b, const rhp_hdr_t &h, const char *name, uint32_t n)
+template <class HV>
+RHP_HD bool name_eq(const HV &hv, uint32_t i, const char *name, uint32_t n)
 {
-  if (h.name_off == RHP_NAME_NULL || h.name_len != n) return false;
+  if (hv.null(i) || hv.name_len(i) != n) return false;
+  const uint8_t *s = hv.name(i);
   uint32_t diff = 0;
-  for (uint32_t i = 0; i < n; i++) diff |= upper(b[h.name_off + i]) ^ upper((uint8_t) name[i]);
+  for (uint32_t k = 0; k < n; k++) diff |= upper(s[k]) ^ upper((uint8_t) name[k]);
   return diff == 0;
 }
 
@@ -186,19 +259,21 @@ RHP_HD void num_step(uint32_t c, uint32_t &st, bool &neg, bool &ovf, uint64_t &v
   v = v * 10 + d;
 }
 
-/* The first kNumWindow bytes are read up front (independent loads); the
- * byte walk continues past them only for longer inputs.  Reading ahead stays
- * inside the request buffer and its RHP_PAD zero tail. */
-RHP_HD uint64_t strtoull10(const uint8_t *s)
+/* strtoull over a header value of n bytes.  Reading stops at the value's end:
+ * a parsed value starts with a byte that is neither OWS nor a CTL, so the
+ * leading-space skip ends inside it, and the byte after it (trimmed OWS, CR or
+ * LF) is no digit -- the same answer as strtoull running on past it.  The first
+ * kNumWindow bytes are read up front (independent loads on the GPU replay). */
+RHP_HD uint64_t strtoull10(const uint8_t *s, uint64_t n)
 {
   constexpr int kNumWindow = 24;
   uint32_t w[kNumWindow];
-  for (int i = 0; i < kNumWindow; i++) w[i] = s[i];
+  for (int i = 0; i < kNumWindow; i++) w[i] = (uint64_t) i < n ? s[i] : 0u;
   uint32_t st = 0;
   bool neg = false, ovf = false;
   uint64_t v = 0;
   for (int i = 0; i < kNumWindow; i++) num_step(w[i], st, neg, ovf, v);
-  for (const uint8_t *q = s + kNumWindow; st != 2; q++) num_step(*q, st, neg, ovf, v);
+  for (uint64_t i = kNumWindow; st != 2 && i < n; i++) num_step(s[i], st, neg, ovf, v);
   return ovf ? ~0ull : neg ? 0 - v : v;
 }
 
@@ -268,42 +343,40 @@ RHP_HD int64_t dechunk(uint8_t *in, uint64_t size, uint64_t *body_len)
   return (int64_t) off;
 }
 
-/* Framing decision given a successful phr parse (n = r.ret > 0). */
-/* cand: the header indices whose name could be Transfer-Encoding or
+/* Framing decision given a successful phr parse (n = ret > 0) of a request of
+ * len bytes at b: get = the method is "GET"; hv / nh = its headers.
+ * cand: the header indices whose name could be Transfer-Encoding or
  * Content-Length (name length 17 or 14), as found by the kernel's decode; ~0
  * checks every header */
-RHP_HD void http_frame(uint8_t *b, uint64_t len, const rhp_req_t &r, const rhp_hdr_t *h, rhp_http_t *x,
-                       uint64_t cand = ~0ull)
+template <class HV>
+RHP_HD void http_frame_t(uint8_t *b, uint64_t len, int64_t n, bool get, const HV &hv, uint32_t nh, rhp_http_t *x,
+                         uint64_t cand = ~0ull)
 {
-  const int64_t n = r.ret;
-  /* one framing candidate (the common case): its record is read together
-   * with the method bytes, and its name together with its value digits, so
-   * the GPU replay makes two memory round trips here instead of five */
+  /* one framing candidate (the common case): its name is read together with
+   * its value digits, so the GPU replay makes fewer memory round trips */
   const bool one = cand != 0 && (cand & (cand - 1)) == 0;
   const uint32_t c = one ? (uint32_t) __builtin_ctzll(cand) : 0u;
-  rhp_hdr_t hc = {0, 0, 0, 0};
-  if (one && c < r.num_headers) hc = h[c];
-  const bool get = r.method_len == 3 && ((b[r.method_off] == 'G') & (b[r.method_off + 1] == 'E') & (b[r.method_off + 2] == 'T'));
   x->result = 1; x->body_kind = 0; x->consumed = (uint64_t) n; x->body_len = 0;
   if (get) return;                                /* GET fast path (http.c:198-202) */
   int te = -1, cl = -1;
   uint64_t size = 0;
   if (one) {
-    if (c < r.num_headers) {
-      size = hc.value_len ? strtoull10(b + hc.value_off) : 0;   /* used only if the name is Content-Length */
-      if (name_eq(b, hc, "Transfer-Encoding", 17)) te = (int) c;
-      if (name_eq(b, hc, "Content-Length", 14)) cl = (int) c;
+    if (c < nh) {
+      const uint64_t vl = hv.value_len(c);
+      size = vl ? strtoull10(hv.value(c), vl) : 0;   /* used only if the name is Content-Length */
+      if (name_eq(hv, c, "Transfer-Encoding", 17)) te = (int) c;
+      if (name_eq(hv, c, "Content-Length", 14)) cl = (int) c;
     }
   } else {
-    for (uint32_t i = 0; i < r.num_headers; i++) {
+    for (uint32_t i = 0; i < nh; i++) {
       if (i < 64 && !((cand >> i) & 1u)) continue;
-      if (te < 0 && name_eq(b, h[i], "Transfer-Encoding", 17)) te = (int) i;
-      if (cl < 0 && name_eq(b, h[i], "Content-Length", 14)) cl = (int) i;
+      if (te < 0 && name_eq(hv, i, "Transfer-Encoding", 17)) te = (int) i;
+      if (cl < 0 && name_eq(hv, i, "Content-Length", 14)) cl = (int) i;
     }
-    if (cl >= 0 && h[cl].value_len != 0) size = strtoull10(b + h[cl].value_off);
+    if (cl >= 0 && hv.value_len((uint32_t) cl) != 0) size = strtoull10(hv.value((uint32_t) cl), hv.value_len((uint32_t) cl));
   }
-  const bool te_set = te >= 0 && (one ? hc.value_len : h[te].value_len) != 0;
-  const bool cl_set = cl >= 0 && (one ? hc.value_len : h[cl].value_len) != 0;
+  const bool te_set = te >= 0 && hv.value_len((uint32_t) te) != 0;
+  const bool cl_set = cl >= 0 && hv.value_len((uint32_t) cl) != 0;
   if (cl_set) {
     if (te_set) { x->result = -1; x->consumed = 0; return; }
     if (len < (uint64_t) n + size) { x->result = 0; x->consumed = 0; return; }
@@ -312,9 +385,10 @@ RHP_HD void http_frame(uint8_t *b, uint64_t len, const rhp_req_t &r, const rhp_h
   }
   if (te_set) {
     const char *ch = "CHUNKED";
-    uint32_t diff = h[te].value_len ^ 7u;
-    for (uint32_t i = 0; i < 7; i++) diff |= upper(b[h[te].value_off + i]) ^ (uint32_t) ch[i];
-    const bool eq = diff == 0;
+    const uint8_t *v = hv.value((uint32_t) te);
+    const uint64_t vl = hv.value_len((uint32_t) te);
+    bool eq = vl == 7u;
+    for (uint32_t i = 0; eq && i < 7; i++) eq = upper(v[i]) == (uint32_t) ch[i];
     if (!eq) { x->result = -1; x->consumed = 0; return; }
     uint64_t blen = 0;
     int64_t size = dechunk(b + n, len - (uint64_t) n, &blen);
@@ -323,6 +397,18 @@ RHP_HD void http_frame(uint8_t *b, uint64_t len, const rhp_req_t &r, const rhp_h
   }
 }
 
+RHP_HD void http_frame(uint8_t *b, uint64_t len, const rhp_req_t &r, const rhp_hdr_t *h, rhp_http_t *x,
+                       uint64_t cand = ~0ull)
+{
+  const bool get = r.method_len == 3 && ((b[r.method_off] == 'G') & (b[r.method_off + 1] == 'E') & (b[r.method_off + 2] == 'T'));
+  http_frame_t(b, len, r.ret, get, HdrsRec{b, h}, r.num_headers, x, cand);
+}
+
+/* phr status -> http_read_request result when the parse gave no request
+ * (http.c:194-195); RHP_RET_TOOLONG (records cannot hold the request) is passed
+ * on for the caller to parse it with a pointer-based parser */
+RHP_HD int32_t http_result_of(int n) { return n == kBad ? -1 : n == RHP_RET_TOOLONG ? RHP_RET_TOOLONG : 0; }
+
 /* Whole http_read_request for one request. */
 template <class Bytes>
 RHP_HD void scalar_http_t(Bytes &B, uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, rhp_http_t *x)
@@ -330,7 +416,7 @@ RHP_HD void scalar_http_t(Bytes &B, uint8_t *b, uint64_t len, uint32_t max, rhp_
   int n = scalar_phr_t(B, len, max, r, h);
   x->body_kind = 0; x->consumed = 0; x->body_len = 0;
   if (len == 0) { x->result = 0; return; }
-  if (n <= 0) { x->result = n == kBad ? -1 : 0; return; }
+  if (n <= 0) { x->result = http_result_of(n); return; }
   http_frame(b, len, *r, h, x);
 }
 RHP_HD void scalar_http(uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, rhp_http_t *x)

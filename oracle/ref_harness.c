@@ -24,14 +24,14 @@ static void ref_canon(orc_req_t *r, orc_hdr_t *h, uint32_t max_headers)
   memset(h, 0, sizeof *h * max_headers);
 }
 
-static int ref_phr_one(const uint8_t *buf, size_t len, orc_req_t *req, orc_hdr_t *hdrs,
-                       uint32_t max_headers, struct phr_header *tmp)
+static int ref_phr_one_last(const uint8_t *buf, size_t len, orc_req_t *req, orc_hdr_t *hdrs,
+                            uint32_t max_headers, struct phr_header *tmp, size_t last_len)
 {
   const char *method, *path;
   size_t method_len, path_len, num = max_headers;
   int minor;
   int r = phr_parse_request((const char *) buf, len, &method, &method_len, &path, &path_len, &minor,
-                            tmp, &num, 0);
+                            tmp, &num, last_len);
   memset(req, 0, sizeof *req);
   req->ret = r;
   if (r > 0) {
@@ -49,6 +49,30 @@ static int ref_phr_one(const uint8_t *buf, size_t len, orc_req_t *req, orc_hdr_t
     }
   }
   return r;
+}
+
+static int ref_phr_one(const uint8_t *buf, size_t len, orc_req_t *req, orc_hdr_t *hdrs,
+                       uint32_t max_headers, struct phr_header *tmp)
+{
+  return ref_phr_one_last(buf, len, req, hdrs, max_headers, tmp, 0);
+}
+
+/* phr_parse_request with a per-request last_len (is_complete runs first when it
+ * is not 0, picohttpparser.c:197-223, 399-401) */
+void ref_phr_batch_last(const uint8_t *bytes, const uint64_t *offsets, const uint64_t *last_len, uint32_t n,
+                        uint32_t max_headers, orc_req_t *reqs, orc_hdr_t *hdrs)
+{
+  struct phr_header tmp[256];
+  if (max_headers > 256)
+    max_headers = 256;
+  for (uint32_t i = 0; i < n; i++) {
+    orc_hdr_t *h = hdrs + (size_t) i * max_headers;
+    memset(h, 0, sizeof *h * max_headers);
+    int r = ref_phr_one_last(bytes + offsets[i], offsets[i + 1] - offsets[i], &reqs[i], h, max_headers, tmp,
+                             last_len[i]);
+    if (r <= 0)
+      ref_canon(&reqs[i], h, max_headers);
+  }
 }
 
 void ref_phr_batch(const uint8_t *bytes, const uint64_t *offsets, uint32_t n,
@@ -215,4 +239,62 @@ uint64_t ref_write_responses(const uint8_t *arena, const uint32_t *resps, const 
   out_off[n] = o;
   stream_destruct(&s);
   return o;
+}
+
+/* http_read_request over a stream per request (config 5's path, http.c:177-234),
+ * threads x reps, on a private copy per thread (chunked bodies are rewritten in
+ * place); returns elapsed ns */
+struct ref_http_mt_arg {
+  uint8_t *bytes;
+  const uint64_t *offsets;
+  uint32_t lo, hi, max_headers;
+  int reps;
+  long sum;
+};
+
+static void *ref_http_mt_worker(void *p)
+{
+  struct ref_http_mt_arg *a = p;
+  http_field_t fields[256];
+  long sum = 0;
+  for (int rep = 0; rep < a->reps; rep++)
+    for (uint32_t i = a->lo; i < a->hi; i++) {
+      stream_t s;
+      memset(&s, 0, sizeof s);
+      s.fd = -1;
+      s.input.data = data(a->bytes + a->offsets[i], a->offsets[i + 1] - a->offsets[i]);
+      s.input.capacity = a->offsets[i + 1] - a->offsets[i];
+      string_t method, target;
+      data_t body;
+      size_t count = a->max_headers;
+      sum += http_read_request(&s, &method, &target, &body, fields, &count) + (long) s.input_consumed;
+    }
+  a->sum = sum;
+  return NULL;
+}
+
+uint64_t ref_http_batch_mt(uint8_t *bytes, const uint64_t *offsets, uint32_t n, uint32_t max_headers,
+                           int threads, int reps, long *checksum)
+{
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  if (max_headers > 256) max_headers = 256;
+  pthread_t tid[256];
+  struct ref_http_mt_arg args[256];
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int t = 0; t < threads; t++) {
+    args[t] = (struct ref_http_mt_arg) {bytes, offsets, (uint32_t) ((uint64_t) n * t / threads),
+                                        (uint32_t) ((uint64_t) n * (t + 1) / threads), max_headers, reps, 0};
+    pthread_create(&tid[t], NULL, ref_http_mt_worker, &args[t]);
+  }
+  long sum = 0;
+  for (int t = 0; t < threads; t++) {
+    pthread_join(tid[t], NULL);
+    sum += args[t].sum;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  if (checksum)
+    *checksum = sum;
+  return (uint64_t) (t1.tv_sec - t0.tv_sec) * 1000000000ull + (uint64_t) (t1.tv_nsec - t0.tv_nsec);
 }

@@ -1,0 +1,75 @@
+"""Hand-built request batches shared by the CPU and GPU tests and by
+tests/golden/make_golden.py (builder sets): the batch contract's edge cases,
+dense header lines, and inputs longer than 64 KiB."""
+from __future__ import annotations
+
+import numpy as np
+
+import libreactorng_amd as rhp
+
+
+def pack(reqs, pad=rhp.RHP_PAD, align_shift=0):
+    parts = [bytes(r) for r in reqs]
+    off = np.zeros(len(parts) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(p) for p in parts])
+    off += align_shift
+    buf = np.zeros(int(off[-1]) + pad, dtype=np.uint8)
+    buf[align_shift:int(off[-1])] = np.frombuffer(b"".join(parts), dtype=np.uint8)
+    return buf, off
+
+
+EDGE = [
+    b"", b"G", b"GET", b"GET ", b"GET  ", b" ", b"GET /", b"GET / ", b"\r", b"\n", b"\r\n", b"\r\nGET ",
+    b"GET / HTTP/1.1\r\n\r\n", b"GET / HTTP/1.1\n\n", b"\r\nGET / HTTP/1.1\r\n\r\n", b"\nGET / HTTP/1.0\n\n",
+    b"GET / HTTP/1.10\r\n\r\n", b"GET / HTTP/1.1\r\nA: b\r\n \tfolded  \r\n\r\n", b"GET / HTTP/1.1\r\nA :b\r\n\r\n",
+    b"GET / HTTP/1.1\r\n:b\r\n\r\n", b"GET / HTTP/1.1\r\nA:\r\n\r\n", b"GET / HTTP/1.1\r\nA: \t \r\n\r\n",
+    b"GET / HTTP/1.1\r\nA: x \t\r\n\r\n", b"GET / HTTP/1.1\r\nA: \x80\xff \r\n\r\n", b"GET / HTTP/1.1\r\nA: a\rb\r\n\r\n",
+    b"GET / HTTP/1.1\r\nA: a\x7fb\r\n\r\n", b"GET \x80\xfe HTTP/1.1\r\n\r\n", b"\x80 / HTTP/1.1\r\n\r\n",
+    b"GET / HTTP/1.1\r\n\r\nGET / HTTP/1.1\r\n\r\n", b"POST / HTTP/1.1\r\nContent-Length: 3\r\n\r\nabc",
+    b"GET / HTTP/1.1\r", b"GET / HTTP/1.1\r\nA: b\r", b"GET / HTTP/1.1\r\nA: b\r\n\r",
+    b"  / HTTP/1.1\r\n\r\n", b"GET  /  HTTP/1.1\r\n\r\n", b"GET / H\r\n\r\n",
+]
+
+
+def dense_header_batch(n=3000, seed=5):
+    """Adversarial: many 3-byte header lines ("a:\n") so up to 6 header records
+    start inside one 16-byte check interval (capture-ring wrap, request-line
+    clobber rule, flush ordering; rhp_dfa.h)."""
+    rng = np.random.default_rng(seed)
+    reqs = []
+    for _ in range(n):
+        rl = (b"GET /" + b"p" * int(rng.integers(0, 40)) + b" HTTP/1." + bytes([48 + int(rng.integers(0, 10))]) +
+              (b"\r\n" if rng.random() < .5 else b"\n"))
+        hs = b"".join((b"a:\n" if rng.random() < .6 else b"bb: v \r\n" if rng.random() < .5 else b"c:\r\n")
+                      for _ in range(int(rng.integers(0, 40))))
+        reqs.append(rl + hs + (b"\r\n" if rng.random() < .9 else b""))
+    return reqs
+
+
+def long_batch():
+    """Inputs longer than 64 KiB: bodies and pipelines past
+    the u16 record range are parsed exactly; only a header section longer than
+    65535 B is RHP_RET_TOOLONG.  Reference: http.c:177-234 (no size limit),
+    buffer.c:56-64 (buffers grow without bound)."""
+    def post(n):
+        return b"POST /upload HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n" % n
+    get = b"GET /plaintext HTTP/1.1\r\nHost: tfb\r\n\r\n"
+    chunks = b"".join(b"%x\r\n%s\r\n" % (4000, b"c" * 4000) for _ in range(20)) + b"0\r\n\r\n"
+    return [
+        post(200000) + b"x" * 200000,                       # 200 KB Content-Length POST
+        post(1 << 20) + b"y" * (1 << 20),                   # 1 MiB POST
+        post(200000) + b"x" * 150000,                       # body still arriving -> http 0
+        get * (72000 // len(get)),                          # ~70 KiB of pipelined GETs
+        get + b"\x00" * 70000,                              # 70 KB after a complete GET
+        b"GET /" + b"a" * 70000 + b" HTTP/1.1\r\n\r\n",      # header section > 64 KiB: TOOLONG
+        b"GET / HTTP/1.1\r\nX: " + b"v" * 70000 + b"\r\n\r\n",  # ... in a value: TOOLONG
+        b"GET / HTTP/1.1\r\nX: " + b"v" * 70000,              # incomplete past 64 KiB -> -2
+        b"GET / HTTP/1.1\r\nX: " + b"v" * 70000 + b"\x01\r\n\r\n",  # CTL past 64 KiB -> -1
+        b"GET / HTTP/1.1\r\n" + b"".join(b"H%d: %s\r\n" % (i, b"z" * 5000) for i in range(20)) + b"\r\n",
+        b"POST /c HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n" + chunks,   # 80 KB chunked body
+        b"POST /c HTTP/1.1\r\nContent-Length: 70000\r\n\r\n" + b"b" * 69999,   # one byte short -> 0
+        b"PUT /q HTTP/1.0\r\nContent-Length: 99999999999999999999999\r\n\r\n" + b"q" * 66000,
+    ]
+
+
+BUILDERS = {"long_batch": long_batch, "edge": lambda: EDGE * 3, "dense": lambda: dense_header_batch(2000, 21)}

@@ -92,10 +92,13 @@ def to_rhp(reqs, hdrs, http, mode):
     n = len(reqs)
     maxh = hdrs.shape[1]
     out = np.zeros(n, dtype=rhp.REQ_DTYPE)
-    ok = reqs["ret"] > 0
+    # a successful parse whose header section exceeds the u16 records is
+    # RHP_RET_TOOLONG in the batch format (include/rhp.h)
+    toolong = reqs["ret"] > rhp.RHP_MAX_LEN
+    ok = (reqs["ret"] > 0) & ~toolong
     if mode == rhp.MODE_HTTP:
         ok &= http["result"] == 1
-    out["ret"] = reqs["ret"]
+    out["ret"] = np.where(toolong, rhp.RHP_RET_TOOLONG, reqs["ret"])
     out["method_off"][ok] = reqs["method_off"][ok]
     out["method_len"][ok] = reqs["method_len"][ok]
     out["path_off"][ok] = reqs["path_off"][ok]
@@ -113,13 +116,14 @@ def to_rhp(reqs, hdrs, http, mode):
     x = None
     if mode == rhp.MODE_HTTP:
         x = np.zeros(n, dtype=rhp.HTTP_DTYPE)
-        x["result"] = http["result"]
-        one = http["result"] == 1
+        x["result"] = np.where(toolong, rhp.RHP_RET_TOOLONG, http["result"])
+        one = (http["result"] == 1) & ~toolong
         x["body_kind"][one] = http["body_kind"][one]
         x["consumed"][one] = http["consumed"][one]
         x["body_len"][one] = http["body_len"][one]
         assert np.all(http["body_off"][one & (http["body_kind"] == 1)] ==
                       reqs["ret"][one & (http["body_kind"] == 1)])
+        # bytes_out: a TOOLONG request's chunked body is not de-framed by the batch parser
     return out, h, x
 
 

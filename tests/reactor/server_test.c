@@ -64,6 +64,17 @@ static void server_callback(reactor_event_t *event)
     reactor_next(server_next2, session);
   else if (string_equal(session->request.target, string("/body")))
     server_plain(session, session->request.body, NULL, 0);   /* echo the request body */
+  else if (string_equal(session->request.target, string("/len")))
+  {
+    /* the body's length and a checksum of its bytes (large bodies) */
+    char text[64];
+    const unsigned char *b = data_base(session->request.body);
+    unsigned long sum = 0;
+    for (size_t i = 0; i < data_size(session->request.body); i++)
+      sum = sum * 31 + b[i];
+    snprintf(text, sizeof text, "%zu %lu", data_size(session->request.body), sum);
+    server_plain(session, string(text), NULL, 0);
+  }
   else
     server_plain(session, string("ok"), NULL, 0);
 }
@@ -158,8 +169,10 @@ static int at_eof(int c, reader_t *r)
   return n == 0;
 }
 
-/* one case: send `req`, expect `responses` 200s with body `want` (NULL: any), then EOF or not */
-static void run_case(const char *name, const char *req, int responses, const char *want, int expect_eof)
+/* one case: send `req` (`n` bytes, in writes of at most `piece` bytes, 0: one
+ * write), expect `responses` 200s with body `want` (NULL: any), then EOF or not */
+static void run_case_n(const char *name, const char *req, size_t n, size_t piece, int responses, const char *want,
+                       int expect_eof)
 {
   static reader_t r;
   char body[256];
@@ -169,8 +182,14 @@ static void run_case(const char *name, const char *req, int responses, const cha
     return;
   r.len = 0;
   r.eof = 0;
-  if (req)
-    send_all(c, req, strlen(req));
+  for (size_t at = 0; req && at < n;)
+  {
+    size_t k = piece && n - at > piece ? piece : n - at;
+    send_all(c, req + at, k);
+    at += k;
+    if (piece)
+      usleep(2000);
+  }
   int got = 0;
   for (int i = 0; i < responses; i++)
   {
@@ -187,6 +206,62 @@ static void run_case(const char *name, const char *req, int responses, const cha
   usleep(20000);
   printf("case %-22s responses %d  callbacks %ld\n", name, got, atomic_load(&calls) - before);
   fflush(stdout);
+}
+
+static void run_case(const char *name, const char *req, int responses, const char *want, int expect_eof)
+{
+  run_case_n(name, req, req ? strlen(req) : 0, 0, responses, want, expect_eof);
+}
+
+/* a POST /len request with an n-byte body of 'x' .. 'z' */
+static char *big_post(size_t n, size_t *total, char *want, size_t want_cap)
+{
+  char head[128];
+  int h = snprintf(head, sizeof head, "POST /len HTTP/1.1\r\nHost: x\r\nContent-Length: %zu\r\n\r\n", n);
+  char *req = malloc((size_t) h + n + 1);
+  memcpy(req, head, (size_t) h);
+  unsigned long sum = 0;
+  for (size_t i = 0; i < n; i++)
+  {
+    req[h + i] = (char) ('x' + i % 3);
+    sum = sum * 31 + (unsigned char) req[h + i];
+  }
+  req[h + n] = 0;
+  *total = (size_t) h + n;
+  snprintf(want, want_cap, "%zu %lu", n, sum);
+  return req;
+}
+
+/* inputs longer than 64 KiB (the reference parses any
+ * length, http.c:177-234, buffer.c:56-64) */
+static void long_cases(void)
+{
+  char want[64];
+  size_t n;
+  char *req = big_post(200000, &n, want, sizeof want);
+  run_case_n("post 200 KB", req, n, 0, 1, want, 0);
+  free(req);
+  req = big_post(1u << 20, &n, want, sizeof want);
+  run_case_n("post 1 MiB in 16 KiB", req, n, 16384, 1, want, 0);
+  free(req);
+  /* ~70 KiB of pipelined GETs in one write */
+  const char get[] = "GET /plaintext HTTP/1.1\r\nHost: tfb\r\n\r\n";
+  const size_t one = sizeof get - 1, count = 72000 / one;
+  req = malloc(one * count + 1);
+  for (size_t i = 0; i < count; i++)
+    memcpy(req + one * i, get, one);
+  req[one * count] = 0;
+  run_case_n("pipelined 70 KiB GETs", req, one * count, 0, (int) count, "ok", 0);
+  free(req);
+  /* a header section longer than the batch records hold (RHP_RET_TOOLONG) */
+  const char pre[] = "GET / HTTP/1.1\r\nX-Big: ";
+  const size_t v = 70000;
+  req = malloc(sizeof pre - 1 + v + 5);
+  memcpy(req, pre, sizeof pre - 1);
+  memset(req + sizeof pre - 1, 'v', v);
+  memcpy(req + sizeof pre - 1 + v, "\r\n\r\n", 5);
+  run_case_n("header section 70 KB", req, sizeof pre - 1 + v + 4, 0, 1, "ok", 0);
+  free(req);
 }
 
 static const char tfb[] = "GET /plaintext HTTP/1.1\r\nHost: tfb-server:8080\r\nAccept: text/plain\r\n"
@@ -249,6 +324,7 @@ static void *client_main(void *unused)
   run_case("post chunked", "POST /body HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n5\r\nhello\r\n6\r\n world\r\n0\r\n\r\n",
            1, "hello world", 0);
   run_case("lf line ends x2", "GET / HTTP/1.1\n\nGET / HTTP/1.1\n\n", 2, "ok", 0);
+  long_cases();
   /* load: many connections, pipelined */
   {
     pthread_t t[256];

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import libreactorng_amd as rhp
+from batches import EDGE, dense_header_batch, long_batch, pack  # noqa: F401
 from oracle_util import assert_same, canon, run_oracle, to_rhp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -93,29 +94,6 @@ def test_dfa_emulation_fuzz_vs_oracle(seed, maxh):
         assert_same(canon(res, mode), want, buf, off, f"emu cfg{cfg} seed{seed} maxh{maxh}")
 
 
-def pack(reqs, pad=rhp.RHP_PAD, align_shift=0):
-    parts = [bytes(r) for r in reqs]
-    off = np.zeros(len(parts) + 1, dtype=np.uint64)
-    off[1:] = np.cumsum([len(p) for p in parts])
-    off += align_shift
-    buf = np.zeros(int(off[-1]) + pad, dtype=np.uint8)
-    buf[align_shift:int(off[-1])] = np.frombuffer(b"".join(parts), dtype=np.uint8)
-    return buf, off
-
-
-EDGE = [
-    b"", b"G", b"GET", b"GET ", b"GET  ", b" ", b"GET /", b"GET / ", b"\r", b"\n", b"\r\n", b"\r\nGET ",
-    b"GET / HTTP/1.1\r\n\r\n", b"GET / HTTP/1.1\n\n", b"\r\nGET / HTTP/1.1\r\n\r\n", b"\nGET / HTTP/1.0\n\n",
-    b"GET / HTTP/1.10\r\n\r\n", b"GET / HTTP/1.1\r\nA: b\r\n \tfolded  \r\n\r\n", b"GET / HTTP/1.1\r\nA :b\r\n\r\n",
-    b"GET / HTTP/1.1\r\n:b\r\n\r\n", b"GET / HTTP/1.1\r\nA:\r\n\r\n", b"GET / HTTP/1.1\r\nA: \t \r\n\r\n",
-    b"GET / HTTP/1.1\r\nA: x \t\r\n\r\n", b"GET / HTTP/1.1\r\nA: \x80\xff \r\n\r\n", b"GET / HTTP/1.1\r\nA: a\rb\r\n\r\n",
-    b"GET / HTTP/1.1\r\nA: a\x7fb\r\n\r\n", b"GET \x80\xfe HTTP/1.1\r\n\r\n", b"\x80 / HTTP/1.1\r\n\r\n",
-    b"GET / HTTP/1.1\r\n\r\nGET / HTTP/1.1\r\n\r\n", b"POST / HTTP/1.1\r\nContent-Length: 3\r\n\r\nabc",
-    b"GET / HTTP/1.1\r", b"GET / HTTP/1.1\r\nA: b\r", b"GET / HTTP/1.1\r\nA: b\r\n\r",
-    b"  / HTTP/1.1\r\n\r\n", b"GET  /  HTTP/1.1\r\n\r\n", b"GET / H\r\n\r\n",
-]
-
-
 @pytest.mark.parametrize("shift", [0, 1, 2, 3])
 @pytest.mark.parametrize("maxh", [0, 1, 16])
 def test_edge_cases_emulation(shift, maxh):
@@ -138,25 +116,50 @@ def test_max_headers_boundary():
 
 
 def test_toolong_request_reported():
+    """A header section longer than the u16 records (ret > 65535) is the one
+    answer the batch format cannot carry: RHP_RET_TOOLONG (include/rhp.h)."""
     big = b"GET /" + b"a" * 70000 + b" HTTP/1.1\r\n\r\n"
     buf, off = pack([b"GET / HTTP/1.1\r\n\r\n", big])
     res, _ = rhp.emulate(buf, off, 16)
     assert res.reqs["ret"][0] == 18 and res.reqs["ret"][1] == rhp.RHP_RET_TOOLONG
+    # the pointer-based host parser has no such limit
+    assert rhp.phr_parse_request_cpu(buf, int(off[1]), len(big), 16)[0] == len(big)
 
 
-def dense_header_batch(n=3000, seed=5):
-    """Adversarial: many 3-byte header lines ("a:\n") so up to 6 header records
-    start inside one 16-byte check interval (capture-ring wrap, request-line
-    clobber rule, flush ordering; rhp_dfa.h)."""
-    rng = np.random.default_rng(seed)
-    reqs = []
-    for _ in range(n):
-        rl = (b"GET /" + b"p" * int(rng.integers(0, 40)) + b" HTTP/1." + bytes([48 + int(rng.integers(0, 10))]) +
-              (b"\r\n" if rng.random() < .5 else b"\n"))
-        hs = b"".join((b"a:\n" if rng.random() < .6 else b"bb: v \r\n" if rng.random() < .5 else b"c:\r\n")
-                      for _ in range(int(rng.integers(0, 40))))
-        reqs.append(rl + hs + (b"\r\n" if rng.random() < .9 else b""))
-    return reqs
+@pytest.mark.parametrize("maxh", [4, 16, 64])
+def test_long_inputs_emulation_and_host_vs_oracle(maxh):
+    buf, off = pack(long_batch())
+    for mode in (rhp.MODE_PHR, rhp.MODE_HTTP):
+        want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
+        res, _ = rhp.emulate(buf, off, maxh, mode)
+        assert_same(canon(res, mode), want, buf, off, f"long inputs emulation maxh{maxh} mode{mode}")
+        res = rhp.parse_cpu_exact(buf, off, maxh, mode)
+        assert_same(canon(res, mode), want, buf, off, f"long inputs host exact maxh{maxh} mode{mode}")
+
+
+def test_long_inputs_pointer_parser_vs_oracle():
+    """rhp_phr_parse_request / rhp_http_read_cpu (pointer outputs, no limit)
+    against the oracle's wide records, including header sections > 64 KiB."""
+    buf, off = pack(long_batch())
+    for maxh in (4, 16):
+        reqs, hdrs, _, _ = run_oracle(buf, off, maxh, rhp.MODE_PHR)
+        for i in range(len(off) - 1):
+            got = rhp.phr_parse_request_cpu(buf, int(off[i]), int(off[i + 1] - off[i]), maxh)
+            r = reqs[i]
+            assert got[0] == r["ret"], (i, got[0], r)
+            if r["ret"] > 0:
+                assert got[1] == r["minor_version"]
+                assert got[2] == (r["method_off"], r["method_len"]) and got[3] == (r["path_off"], r["path_len"])
+                want_h = [tuple(int(v) for v in hdrs[i, k]) for k in range(int(r["num_headers"]))]
+                assert got[4] == want_h, i
+        rw = buf.copy()
+        _, _, http, _ = run_oracle(buf, off, maxh, rhp.MODE_HTTP)
+        for i in range(len(off) - 1):
+            res, consumed, body = rhp.http_read_cpu(rw, int(off[i]), int(off[i + 1] - off[i]), maxh)
+            assert res == http["result"][i], (i, res, http[i])
+            if res == 1:
+                assert consumed == http["consumed"][i]
+                assert (body is not None) == bool(http["body_kind"][i])
 
 
 @pytest.mark.parametrize("shift", [0, 3])

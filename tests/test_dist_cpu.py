@@ -55,3 +55,36 @@ def test_shards_partition_and_match_single_process():
     assert np.array_equal(rets, full.reqs["ret"])
     assert alg == rhp.header_bytes(rhp.GEN_ZIPF, N_TOTAL, SEED)
     assert tmax == 1.5
+
+
+def _bench(args, env=None):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=e, capture_output=True,
+                       text=True, timeout=600)
+    lines = [line for line in p.stdout.splitlines() if line.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+def test_bench_launches_its_own_ranks():
+    """`bench.py --gpus 2` without a launcher starts 2 rank processes itself
+    (gloo control plane, contiguous shards, max-over-ranks time, summed bytes);
+    --device cpu runs the kernel's CPU emulation in place of the GPU."""
+    rc, line, err = _bench(["--gpus", "2", "--device", "cpu", "--steps", "2", "--warmup", "1", "--no-cpu",
+                            "--per-gpu", "32768"])
+    assert rc == 0, err
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "shard2"
+    assert line["config"]["global_requests"] == 65536 and line["config"]["requests_per_gpu"] == 32768
+    assert line["config"]["ok_fraction"] == 1.0 and line["value"] > 0
+
+
+def test_bench_rejects_world_size_mismatch():
+    rc, line, _ = _bench(["--gpus", "4", "--device", "cpu", "--steps", "1", "--no-cpu", "--per-gpu", "1024"],
+                         env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc == 2 and line is None

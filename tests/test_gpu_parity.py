@@ -9,19 +9,20 @@ import numpy as np
 import pytest
 
 import libreactorng_amd as rhp
+from golden_sets import inputs, record_digest
 from oracle_util import assert_same, canon, run_oracle, to_rhp
-from test_cpu_units import EDGE, dense_header_batch, pack
+from batches import EDGE, dense_header_batch, long_batch, pack
 
 pytestmark = pytest.mark.gpu
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))["sets"]
+FULL = json.load(open(os.path.join(GOLDEN, "full_digests.json")))["sets"]
 
 
 def golden(name):
     spec = MANIFEST[name]
-    buf, off = rhp.generate(spec["config"], spec["n"], spec["seed"])
-    assert hashlib.sha256(buf.tobytes()).hexdigest() == spec["input_sha256"]
+    buf, off = inputs(spec)
     z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
     return spec, buf, off, (z["reqs"], z["hdrs"], z["http"] if "http" in z.files else None), z
 
@@ -71,13 +72,36 @@ def test_gpu_edge_cases(shift):
 
 
 def test_gpu_toolong_and_empty_batch():
+    """Only a header section longer than the u16 records (ret > 65535) is
+    RHP_RET_TOOLONG; a 70 KB request whose header section is short parses."""
     big = b"GET /" + b"a" * 70000 + b" HTTP/1.1\r\n\r\n"
-    buf, off = pack([b"GET / HTTP/1.1\r\n\r\n", big, b""])
-    res = rhp.parse_batch(buf, off, 16)
-    assert list(res.reqs["ret"]) == [18, rhp.RHP_RET_TOOLONG, -2]
+    long_tail = b"GET / HTTP/1.1\r\n\r\n" + b"x" * 70000
+    buf, off = pack([b"GET / HTTP/1.1\r\n\r\n", big, b"", long_tail])
+    for impl in (rhp.IMPL_DFA, rhp.IMPL_EXACT):
+        res = rhp.parse_batch(buf, off, 16, impl=impl)
+        assert list(res.reqs["ret"]) == [18, rhp.RHP_RET_TOOLONG, -2, 18]
+        res = rhp.parse_batch(buf, off, 16, rhp.MODE_HTTP, impl=impl)
+        assert list(res.http["result"]) == [1, rhp.RHP_RET_TOOLONG, 0, 1]
     buf, off = pack([])
     res = rhp.parse_batch(buf, off, 16)
     assert len(res.reqs) == 0
+
+
+@pytest.mark.parametrize("impl", [rhp.IMPL_DFA, rhp.IMPL_EXACT])
+@pytest.mark.parametrize("shift", [0, 1, 3])
+def test_gpu_long_inputs_vs_oracle(impl, shift):
+    """Inputs past 64 KiB (200 KB / 1 MiB Content-Length POSTs, ~70 KiB of
+    pipelined GETs, chunked bodies, errors and partials past 64 KiB) bit-exact
+    vs the oracle, bytes rewritten in place included."""
+    buf, off = pack(long_batch(), align_shift=shift)
+    for maxh in (4, 16):
+        for mode in (rhp.MODE_PHR, rhp.MODE_HTTP):
+            res = rhp.parse_batch(buf, off, maxh, mode, impl=impl)
+            reqs, hdrs, http, rw = run_oracle(buf, off, maxh, mode)
+            assert_same(canon(res, mode), to_rhp(reqs, hdrs, http, mode), buf, off,
+                        f"GPU long inputs impl{impl} shift{shift} maxh{maxh} mode{mode}")
+            if mode == rhp.MODE_HTTP:
+                assert np.array_equal(res.bytes_out, rw)
 
 
 def test_gpu_repeated_launches_rearm_work_counter():
@@ -132,3 +156,19 @@ def test_gpu_dense_headers(shift):
             res = rhp.parse_batch(buf, off, maxh, mode)
             want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
             assert_same(canon(res, mode), want, buf, off, f"GPU dense shift{shift} maxh{maxh} mode{mode}")
+
+
+@pytest.mark.parametrize("name", sorted(FULL))
+def test_gpu_full_size_matches_reference_digest(name):
+    """BASELINE configs 2, 3 (max_headers 32 and 16), 5 at full size and every
+    shard of config 4 (8M requests over 8 GPUs, shard g = requests [g*2^20,
+    (g+1)*2^20)): the kernel's canonical record stream hashes to the digest of
+    the compiled reference's (tests/golden/full_digests.json)."""
+    spec = FULL[name]
+    buf, off = inputs(spec)
+    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"])
+    got = canon(res, spec["mode"])
+    if record_digest(*got) != spec["records_sha256"]:   # say which request differs
+        want = to_rhp(*run_oracle(buf, off, spec["max_headers"], spec["mode"])[:3], spec["mode"])
+        assert_same(got, want, buf, off, name)
+        raise AssertionError(f"{name}: digest differs from the reference but matches the oracle")

@@ -8,22 +8,24 @@ import numpy as np
 import pytest
 
 import libreactorng_amd as rhp
+from golden_sets import inputs, record_digest
 from oracle_util import assert_same, canon, run_oracle, to_rhp
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))["sets"]
+MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+SETS = MANIFEST["sets"]
+FULL = json.load(open(os.path.join(GOLDEN, "full_digests.json")))["sets"]
 
 
 def load_golden(name):
-    spec = MANIFEST[name]
-    buf, off = rhp.generate(spec["config"], spec["n"], spec["seed"])
-    assert hashlib.sha256(buf.tobytes()).hexdigest() == spec["input_sha256"], "generator drifted"
+    spec = SETS[name]
+    buf, off = inputs(spec)
     z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
     want = (z["reqs"], z["hdrs"], z["http"] if "http" in z.files else None)
     return spec, buf, off, want, z
 
 
-@pytest.mark.parametrize("name", sorted(MANIFEST))
+@pytest.mark.parametrize("name", sorted(SETS))
 def test_oracle_matches_reference_golden(name):
     spec, buf, off, want, z = load_golden(name)
     reqs, hdrs, http, out = run_oracle(buf, off, spec["max_headers"], spec["mode"])
@@ -33,7 +35,7 @@ def test_oracle_matches_reference_golden(name):
         assert hashlib.sha256(out.tobytes()).digest() == z["bytes_out_sha256"].tobytes()
 
 
-@pytest.mark.parametrize("name", sorted(MANIFEST))
+@pytest.mark.parametrize("name", sorted(SETS))
 def test_dfa_emulation_matches_golden(name):
     spec, buf, off, want, z = load_golden(name)
     res, stats = rhp.emulate(buf, off, spec["max_headers"], spec["mode"])
@@ -42,7 +44,7 @@ def test_dfa_emulation_matches_golden(name):
         assert hashlib.sha256(res.bytes_out.tobytes()).digest() == z["bytes_out_sha256"].tobytes()
 
 
-@pytest.mark.parametrize("name", sorted(MANIFEST))
+@pytest.mark.parametrize("name", sorted(SETS))
 def test_cpu_exact_parser_matches_golden(name):
     spec, buf, off, want, z = load_golden(name)
     res = rhp.parse_cpu_exact(buf, off, spec["max_headers"], spec["mode"])
@@ -91,3 +93,47 @@ def test_known_answer_tfb128():
         (25, 4, 31, 15), (48, 6, 56, 10), (68, 10, 80, 10), (92, 10, 104, 20)]
     res, _ = rhp.emulate(buf, off, 16)
     assert_same(canon(res, rhp.MODE_PHR), (r, h, None), buf, off, "KAT emulation")
+
+
+def test_pointer_parser_last_len_matches_reference_golden():
+    """rhp_phr_parse_request (phr_parse_request's signature, pointer outputs) with
+    last_len != 0 -- is_complete first (picohttpparser.c:197-223, 399-401) --
+    against the compiled reference's answers (tests/golden/phr_last_len.npz)."""
+    spec = MANIFEST["phr_last_len"]
+    buf, off = inputs(spec)
+    z = np.load(os.path.join(GOLDEN, "phr_last_len.npz"))
+    for i in range(len(off) - 1):
+        ret, minor, m, p, hs = rhp.phr_parse_request_cpu(buf, int(off[i]), int(off[i + 1] - off[i]), 16,
+                                                         int(z["last_len"][i]))
+        w = z["reqs"][i]
+        assert ret == w["ret"], (i, ret, w)
+        if ret > 0:
+            assert (minor, m, p) == (w["minor_version"], (w["method_off"], w["method_len"]),
+                                     (w["path_off"], w["path_len"])), i
+            want = [(-1 if h["name_off"] == rhp.RHP_NAME_NULL else int(h["name_off"]), int(h["name_len"]),
+                     int(h["value_off"]), int(h["value_len"])) for h in z["hdrs"][i][: int(w["num_headers"])]]
+            assert hs == want, i
+
+
+@pytest.mark.parametrize("name", ["config2_get256_h16", "config5_post1k_http_h16", "config4_get256_shard7of8"])
+def test_oracle_full_size_matches_reference_digest(name):
+    """The restatement at BASELINE full size (1M requests) against the digest of
+    the compiled reference's record stream (tests/golden/full_digests.json)."""
+    spec = FULL[name]
+    buf, off = inputs(spec)
+    got = to_rhp(*run_oracle(buf, off, spec["max_headers"], spec["mode"])[:3], spec["mode"])
+    assert record_digest(*got) == spec["records_sha256"]
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference"), reason="needs the reference sources (dev container)")
+def test_diff_fuzz_oracle_vs_compiled_reference():
+    """A short run of oracle/diff_fuzz.c: the restatement against the reference
+    compiled from /root/reference (every generator config x max_headers, phr
+    and http mode, rewritten bytes included).  The long runs (>= 10^7 requests)
+    are logged under profiles/ by tools/run_diff_fuzz.sh."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.check_call(["make", "-s", "-C", os.path.join(root, "oracle"), "ref"])
+    out = subprocess.run([os.path.join(root, "oracle", "_ref", "diff_fuzz"), "42", "2000", "7"], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0 and "diff_fuzz OK: 84000 requests" in out.stdout, out.stdout + out.stderr

@@ -1,0 +1,40 @@
+#!/bin/bash
+# One GPU session of evidence for the committed kernel: the GPU test suite, the
+# bench line, rocprofv3 kernel-trace summaries of configs 2/3/5 and PMC
+# FETCH_SIZE / WRITE_SIZE passes (separate runs).  Every GPU step has its own
+# time limit; steps are chained with && so a failure stops the session.
+# STEPS=tests,bench,prof,pmc (default all)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out && export TMPDIR=/tmp
+TAG=${TAG:-s}
+STEPS=${STEPS:-tests,bench,prof,pmc}
+has() { [[ ",$STEPS," == *",$1,"* ]]; }
+ok=0
+step_tests() {
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > gpurun_out/pytest_${TAG}.log 2>&1 && echo TESTS_OK && tail -3 gpurun_out/pytest_${TAG}.log
+}
+step_bench() {
+  timeout -k 10 600 python -u bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err \
+    && cat gpurun_out/bench_${TAG}.json
+}
+step_prof() {
+  for c in get256 zipf post; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_${TAG}_$c -o run \
+      -- python3 bench.py --config $c --extra none --steps 30 --warmup 5 --no-cpu > gpurun_out/prof_${TAG}_$c.log 2>&1 \
+      || return 1
+    echo PROF_${c}_OK
+  done
+}
+step_pmc() {
+  for c in get256 zipf post; do
+    for k in FETCH_SIZE WRITE_SIZE; do
+      timeout -k 10 -s KILL 240 rocprofv3 --pmc $k --output-format csv -d gpurun_out/pmc_${TAG}_${c}_$k -o p \
+        -- python3 bench.py --config $c --extra none --steps 6 --warmup 2 --no-cpu > gpurun_out/pmc_${TAG}_${c}_$k.log 2>&1 \
+        || return 1
+    done
+    echo PMC_${c}_OK
+  done
+}
+( ! has tests || step_tests ) && ( ! has bench || step_bench ) && ( ! has prof || step_prof ) && ( ! has pmc || step_pmc ) \
+  && echo SESSION_OK

@@ -221,11 +221,17 @@ class GpuRunner:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(self.stream)
+        t1 = time.perf_counter()
         for k in range(steps):
             self.step(k)
+        t2 = time.perf_counter()
         ev1.record(self.stream)
         torch.cuda.synchronize()
-        return time.perf_counter() - t0, ev0.elapsed_time(ev1) / steps
+        t3 = time.perf_counter()
+        if os.environ.get("RHP_BENCH_DIAG"):
+            print(f"bench diag: record {1e3 * (t1 - t0):.3f} ms, {steps} launches {1e3 * (t2 - t1):.3f} ms, "
+                  f"record+sync {1e3 * (t3 - t2):.3f} ms", file=sys.stderr)
+        return t3 - t0, ev0.elapsed_time(ev1) / steps
 
     def ok_fraction(self):
         res = self.copies[0].result()

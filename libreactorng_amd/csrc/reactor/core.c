@@ -118,6 +118,8 @@ void buffer_append(buffer_t *b, data_t d)
 
 void buffer_erase(buffer_t *b, size_t at, size_t n)
 {
+  if (n == 0)
+    return;
   memmove((char *) buffer_base(b) + at, (char *) buffer_base(b) + at + n, buffer_size(b) - at - n);
   b->data.iov.iov_len -= n;
 }

@@ -74,3 +74,17 @@ def test_server_cases_gpu_batch_parser():
     print(out)
     assert "parser: gpu" in out and "OK (0 failures)" in out
     assert "config1 16 pipelined   responses 16  callbacks 16" in out
+
+
+def test_reactor_host_code_asan_ubsan_clean(tmp_path):
+    """libreactor.so, the host parser library and the two test programs built
+    with -fsanitize=address,undefined (Makefile target `asan`): the reference's
+    http vectors (buffer_append only, as test/http.c:134) and the server cases,
+    long inputs included, run clean, leak check on."""
+    subprocess.check_call(["make", "-s", "-C", os.path.join(LIB, "csrc"), "asan"])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
+    asan = os.path.join(LIB, "asan")
+    for args in ([os.path.join(asan, "http_test"), _vectors(tmp_path)], [os.path.join(asan, "server_test"), "8", "16"]):
+        p = subprocess.run(args, env=dict(env, RHP_REACTOR_PARSER="host"), capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0 and "OK (0 failures)" in p.stdout, p.stdout + p.stderr
+        assert "runtime error" not in p.stderr and "AddressSanitizer" not in p.stderr, p.stderr

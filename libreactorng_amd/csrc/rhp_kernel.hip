@@ -155,6 +155,12 @@ __device__ __forceinline__ uint32_t dma_part(uint32_t w, uint32_t j)     /* ... 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+#ifdef RHP_CLOCK
+/* diagnostic build only: shader ticks and 100 MHz real-time ticks from the
+ * entry of the first wave to its exit, written by block 0 wave 0 (never read
+ * by the kernel); the quotient is the shader clock the kernel ran at */
+__device__ unsigned long long g_clock[2];
+#endif
 #ifdef RHP_STAMPS
 /* diagnostic build only: per-wave cycle sums per loop section (never read by the kernel) */
 __device__ unsigned long long g_stamps[8192 * 8];
@@ -391,6 +397,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
+#ifdef RHP_CLOCK
+  const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef RHP_STAMPS
   const uint32_t wave = tid >> 6;
   unsigned long long t_entry = 0;
@@ -651,6 +660,12 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     uint64_t mh[kEvWords / 2];
 #pragma unroll
     for (int h = 0; h < (int) kEvWords / 2; h++) mh[h] = slow ? 0ull : (((uint64_t) ev[2 * h + 1] << 32) | ev[2 * h]);
+#ifdef RHP_EXP_NODECODE   /* timing experiment: only the terminal is taken from the mask (records left unwritten) */
+    if (!term_ev) {
+#pragma unroll
+      for (int h = 0; h < (int) kEvWords / 2; h++) mh[h] = 0;
+    }
+#endif
     uint32_t term_pos = 0xffffffffu;
     if (term_ev) {   /* the terminal is the block's last event: take it off the mask */
       bool found = false;
@@ -665,6 +680,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       }
     }
     rhp_hdr_t *hout = p.hdrs + (uint64_t) cur * maxh;
+#ifdef RHP_EXP_NODECODE
+#pragma unroll
+    for (int h = 0; h < (int) kEvWords / 2; h++) mh[h] = 0;
+#endif
 #ifdef RHP_DEC32   /* 32-bit event words (experiment) */
 #pragma unroll
     for (int q = 0; q < (int) kEvWords; q++) {
@@ -1137,6 +1156,13 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     }
   }
 #endif
+#ifdef RHP_CLOCK
+  if (blockIdx.x == 0 && tid == 0) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    g_clock[0] = t1 - clk_t0;
+    g_clock[1] = r1 - clk_r0;
+  }
+#endif
 #ifdef RHP_STAMPS
   if (lane == 0) {
     unsigned long long t_end = 0;
@@ -1228,6 +1254,14 @@ int rhp_debug_stamps(unsigned long long *host)
 int rhp_debug_stamps_end(unsigned long long *host)
 {
   return (int) hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps_end), sizeof(g_stamps_end), 0, hipMemcpyDeviceToHost);
+}
+#endif
+
+#ifdef RHP_CLOCK
+/* diagnostic build only: (shader ticks, 100 MHz ticks) of block 0's last launch */
+int rhp_debug_clock(unsigned long long *host)
+{
+  return (int) hipMemcpyFromSymbol(host, HIP_SYMBOL(g_clock), sizeof(g_clock), 0, hipMemcpyDeviceToHost);
 }
 #endif
 

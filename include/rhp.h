@@ -70,6 +70,21 @@ typedef struct rhp_hdr {
 
 #define RHP_NAME_NULL 0xFFFFu
 
+/* Layout of the header records.  Request-major (the C array hdrs[n][max_headers],
+ * the default): a request's records are contiguous.  Header-major
+ * (hdrs[max_headers][n]): the records of one header index are contiguous across
+ * requests, so the records a wave completes together for consecutive requests of
+ * a uniform batch are whole lines (request-major writes them as one partial
+ * line per request, which HBM handles at a fraction of its write rate:
+ * profiles/r02/ubench_records.txt).  Records past num_headers are unspecified. */
+enum rhp_layout {
+  RHP_LAYOUT_REQUEST_MAJOR = 0,
+  RHP_LAYOUT_HEADER_MAJOR = 1
+};
+/* record k of request i in a batch of n requests with capacity m */
+#define RHP_HDR(hdrs, layout, n, m, i, k) \
+  ((hdrs)[(layout) == RHP_LAYOUT_HEADER_MAJOR ? (size_t) (k) * (n) + (i) : (size_t) (i) * (m) + (k)])
+
 /* http_read_request result (24 B), RHP_MODE_HTTP only */
 typedef struct rhp_http {
   int32_t  result;         /* 1 ready, 0 need more bytes / empty, -1 malformed, RHP_RET_TOOLONG */
@@ -88,9 +103,9 @@ typedef struct rhp_batch {
   uint32_t        n;
   uint32_t        max_headers; /* headers capacity per request (*num_headers in) */
   uint32_t        mode;        /* enum rhp_mode */
-  uint32_t        reserved;
+  uint32_t        layout;      /* enum rhp_layout: where record k of request i lives in hdrs */
   rhp_req_t      *reqs;        /* device [n] */
-  rhp_hdr_t      *hdrs;        /* device [n * max_headers] */
+  rhp_hdr_t      *hdrs;        /* device [n * max_headers] records, laid out as `layout` says */
   rhp_http_t     *http;        /* device [n], RHP_MODE_HTTP */
   uint32_t       *work;        /* reserved, may be NULL (device scratch of RHP_WORK_WORDS u32
                                   for future kernels; the current ones keep their scheduling

@@ -27,6 +27,7 @@ RHP_MAX_HEADERS = 64
 RHP_RET_TOOLONG = -3
 RHP_WORK_WORDS = 64
 MODE_PHR, MODE_HTTP = 0, 1
+LAYOUT_REQUEST_MAJOR, LAYOUT_HEADER_MAJOR = 0, 1
 IMPL_DFA, IMPL_EXACT = 0, 1
 RHP_NAME_NULL = 0xFFFF
 F_EXACT = 0x1
@@ -46,7 +47,7 @@ class Batch(ctypes.Structure):
     """struct rhp_batch (include/rhp.h)."""
     _fields_ = [("bytes", ctypes.c_void_p), ("bytes_rw", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
                 ("bytes_size", ctypes.c_uint64), ("n", ctypes.c_uint32), ("max_headers", ctypes.c_uint32),
-                ("mode", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("reqs", ctypes.c_void_p),
+                ("mode", ctypes.c_uint32), ("layout", ctypes.c_uint32), ("reqs", ctypes.c_void_p),
                 ("hdrs", ctypes.c_void_p), ("http", ctypes.c_void_p), ("work", ctypes.c_void_p)]
 
 
@@ -189,25 +190,33 @@ def header_bytes(config: int, n: int, seed: int, lo: int = 0) -> int:
 @dataclass
 class Result:
     reqs: np.ndarray           # REQ_DTYPE [n]
-    hdrs: np.ndarray           # HDR_DTYPE [n, max_headers]
+    hdrs: np.ndarray           # HDR_DTYPE [n, max_headers] (a view of the header-major batch array)
     http: np.ndarray | None    # HTTP_DTYPE [n] (http mode)
     bytes_out: np.ndarray | None = None  # request bytes after http mode (chunked bodies rewritten)
 
 
-def _host_batch(buf, off, max_headers, mode):
+def hdr_view(flat: np.ndarray, n: int, max_headers: int, layout: int) -> np.ndarray:
+    """The [n, max_headers] view of a batch's record array in either layout (include/rhp.h)."""
+    if layout == LAYOUT_HEADER_MAJOR:
+        return flat[: n * max_headers].reshape(max_headers, n).T
+    return flat[: n * max_headers].reshape(n, max_headers)
+
+
+def _host_batch(buf, off, max_headers, mode, layout=LAYOUT_REQUEST_MAJOR):
     n = len(off) - 1
     reqs = np.zeros(n, dtype=REQ_DTYPE)
-    hdrs = np.zeros((n, max(max_headers, 1)), dtype=HDR_DTYPE)
+    hdrs = np.zeros(max(max_headers * n, 1), dtype=HDR_DTYPE)
     http = np.zeros(n, dtype=HTTP_DTYPE)
     rw = buf.copy()
-    b = Batch(_ptr(rw), _ptr(rw), _ptr(off), rw.size, n, max_headers, mode, 0, _ptr(reqs), _ptr(hdrs),
+    b = Batch(_ptr(rw), _ptr(rw), _ptr(off), rw.size, n, max_headers, mode, layout, _ptr(reqs), _ptr(hdrs),
               _ptr(http), 0)
-    return b, Result(reqs, hdrs[:, :max_headers], http if mode == MODE_HTTP else None, rw)
+    return b, Result(reqs, hdr_view(hdrs, n, max_headers, layout), http if mode == MODE_HTTP else None, rw)
 
 
-def emulate(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR):
+def emulate(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,
+            layout: int = LAYOUT_REQUEST_MAJOR):
     """Run the kernel's DFA algorithm on the CPU (tests).  Returns (Result, stats[3])."""
-    b, res = _host_batch(buf, off, max_headers, mode)
+    b, res = _host_batch(buf, off, max_headers, mode, layout)
     stats = np.zeros(3, dtype=np.uint64)
     rc = host().rhp_emu_parse_batch(ctypes.byref(b), _ptr(stats))
     if rc != 0:
@@ -215,9 +224,10 @@ def emulate(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int =
     return res, stats
 
 
-def parse_cpu_exact(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR):
+def parse_cpu_exact(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,
+                    layout: int = LAYOUT_REQUEST_MAJOR):
     """The product's exact scalar parser on the host (rhp_scalar.h), e.g. for the reactor shim."""
-    b, res = _host_batch(buf, off, max_headers, mode)
+    b, res = _host_batch(buf, off, max_headers, mode, layout)
     host().rhp_cpu_parse_batch(ctypes.byref(b))
     return res
 
@@ -226,13 +236,14 @@ class DeviceBatch:
     """A batch resident in HBM plus its output buffers (torch tensors as plumbing)."""
 
     def __init__(self, buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,
-                 device: str = "cuda"):
+                 device: str = "cuda", layout: int = LAYOUT_REQUEST_MAJOR):
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("no GPU visible: the rhp product path runs on MI355X only")
         self.n = len(off) - 1
         self.max_headers = max_headers
         self.mode = mode
+        self.layout = layout
         self.bytes = torch.from_numpy(buf).to(device)
         self.offsets = torch.from_numpy(off.view(np.int64)).to(device)
         self.reqs = torch.zeros(self.n * REQ_DTYPE.itemsize, dtype=torch.uint8, device=device)
@@ -244,7 +255,7 @@ class DeviceBatch:
 
     def desc(self) -> Batch:
         return Batch(self.bytes.data_ptr(), self.bytes.data_ptr(), self.offsets.data_ptr(), self.bytes.numel(),
-                     self.n, self.max_headers, self.mode, 0, self.reqs.data_ptr(), self.hdrs.data_ptr(),
+                     self.n, self.max_headers, self.mode, self.layout, self.reqs.data_ptr(), self.hdrs.data_ptr(),
                      self.http.data_ptr(), self.work.data_ptr())
 
     def launch(self, stream=None) -> None:
@@ -259,19 +270,18 @@ class DeviceBatch:
         import torch
         torch.cuda.synchronize()
         reqs = self.reqs.cpu().numpy().view(REQ_DTYPE)
-        hdrs = self.hdrs.cpu().numpy().view(HDR_DTYPE)[: self.n * self.max_headers]
-        hdrs = hdrs.reshape(self.n, self.max_headers)
+        hdrs = hdr_view(self.hdrs.cpu().numpy().view(HDR_DTYPE), self.n, self.max_headers, self.layout)
         http = self.http.cpu().numpy().view(HTTP_DTYPE) if self.mode == MODE_HTTP else None
         out = self.bytes.cpu().numpy() if self.mode == MODE_HTTP else None
         return Result(reqs, hdrs, http, out)
 
 
 def parse_batch(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,
-                impl: int = IMPL_DFA) -> Result:
+                impl: int = IMPL_DFA, layout: int = LAYOUT_REQUEST_MAJOR) -> Result:
     """Parse a host batch on the GPU (copies in, one launch, copies out)."""
     lib().rhp_set_impl(impl)
     try:
-        db = DeviceBatch(buf, off, max_headers, mode)
+        db = DeviceBatch(buf, off, max_headers, mode, layout=layout)
         db.launch()
         return db.result()
     finally:

@@ -229,6 +229,7 @@ int reactor_batch_run(uint32_t n, size_t bytes, reactor_batch_result_t *out)
   out->bytes = B.h_bytes;
   out->reqs = B.h_req;
   out->hdrs = B.h_hdr;
+  out->n = n;
   out->http = B.h_http;
   return 0;
 }

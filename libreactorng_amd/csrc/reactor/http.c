@@ -35,15 +35,16 @@ string_t http_field_lookup(http_field_t *fields, size_t fields_count, string_t n
 }
 
 /* request records (offsets into `base`) -> the reference's output iovecs */
-void reactor_http_fill(const uint8_t *base, const rhp_req_t *r, const rhp_hdr_t *h, const rhp_http_t *x,
+void reactor_http_fill(const uint8_t *base, const rhp_req_t *r, const rhp_hdr_t *h, size_t hs, const rhp_http_t *x,
                        string_t *method, string_t *target, data_t *body, http_field_t *fields, size_t *fields_count)
 {
   *method = data(base + r->method_off, r->method_len);
   *target = data(base + r->path_off, r->path_len);
   for (uint32_t k = 0; k < r->num_headers; k++)
   {
-    fields[k].name = h[k].name_off == RHP_NAME_NULL ? data_null() : data(base + h[k].name_off, h[k].name_len);
-    fields[k].value = data(base + h[k].value_off, h[k].value_len);
+    const rhp_hdr_t *o = &h[k * hs];   /* header-major batch records (rhp.h) */
+    fields[k].name = o->name_off == RHP_NAME_NULL ? data_null() : data(base + o->name_off, o->name_len);
+    fields[k].value = data(base + o->value_off, o->value_len);
   }
   *fields_count = r->num_headers;
   *body = x->body_kind ? data(base + r->ret, x->body_len) : data_null();

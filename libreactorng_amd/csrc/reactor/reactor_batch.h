@@ -12,7 +12,8 @@ typedef struct reactor_batch_result
 {
   const uint8_t    *bytes;   /* the packed input after the parse (chunked bodies de-framed) */
   const rhp_req_t  *reqs;
-  const rhp_hdr_t  *hdrs;    /* REACTOR_BATCH_HEADERS per request */
+  const rhp_hdr_t  *hdrs;    /* REACTOR_BATCH_HEADERS per request, header-major (stride n) */
+  uint32_t          n;
   const rhp_http_t *http;
 } reactor_batch_result_t;
 
@@ -24,7 +25,7 @@ int       reactor_batch_run(uint32_t n, size_t bytes, reactor_batch_result_t *ou
 
 /* records (offsets into base) -> the reference's output iovecs (http.c) */
 struct http_field;
-void reactor_http_fill(const uint8_t *base, const rhp_req_t *r, const rhp_hdr_t *h, const rhp_http_t *x,
+void reactor_http_fill(const uint8_t *base, const rhp_req_t *r, const rhp_hdr_t *h, size_t hs, const rhp_http_t *x,
                        data_t *method, data_t *target, data_t *body, struct http_field *fields, size_t *fields_count);
 
 #endif

@@ -253,7 +253,7 @@ static bool server_session_dispatch(server_session_t *s, const piece_t *pc, size
       uint8_t *base = data_base(in);
       if (x->body_kind && x->consumed != (uint64_t) res->reqs[p->index].ret + x->body_len)
         memcpy(base, res->bytes + off, x->consumed);   /* chunked body, de-framed in place */
-      reactor_http_fill(base, &res->reqs[p->index], res->hdrs + (size_t) p->index * REACTOR_BATCH_HEADERS, x,
+      reactor_http_fill(base, &res->reqs[p->index], res->hdrs + (size_t) p->index * REACTOR_BATCH_HEADERS, 1, x,
                         &s->request.method, &s->request.target, &s->request.body, s->request.fields,
                         &s->request.fields_count);
       consumed = x->consumed;

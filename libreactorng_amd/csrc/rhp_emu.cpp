@@ -35,9 +35,11 @@ void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
 {
   rhp_req_t r;
   r.flags = RHP_F_EXACT;
-  rhp_hdr_t *h = b->hdrs + (uint64_t) i * b->max_headers;
-  if (b->mode == RHP_MODE_HTTP) scalar_http(b->bytes_rw + off, len, b->max_headers, &r, h, &b->http[i]);
-  else scalar_phr(b->bytes + off, len, b->max_headers, &r, h);
+  const uint64_t hs_req = b->layout == RHP_LAYOUT_HEADER_MAJOR ? 1u : b->max_headers;
+  const uint64_t hs_hdr = b->layout == RHP_LAYOUT_HEADER_MAJOR ? b->n : 1u;
+  rhp_hdr_t *h = b->hdrs + i * hs_req;
+  if (b->mode == RHP_MODE_HTTP) scalar_http(b->bytes_rw + off, len, b->max_headers, &r, h, hs_hdr, &b->http[i]);
+  else scalar_phr(b->bytes + off, len, b->max_headers, &r, h, hs_hdr);
   b->reqs[i] = r;
 }
 
@@ -59,7 +61,9 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
     uint32_t st = idx2(s0, 0);
     Dec d;
     dec_reset(d);
-    rhp_hdr_t *hout = b->hdrs + (uint64_t) i * maxh;
+    const uint64_t hs_req = b->layout == RHP_LAYOUT_HEADER_MAJOR ? 1u : maxh;
+    const uint64_t hs_hdr = b->layout == RHP_LAYOUT_HEADER_MAJOR ? b->n : 1u;
+    rhp_hdr_t *hout = b->hdrs + i * hs_req;
     for (;;) {
       /* one RHP_BLOCK-byte block: steps, then the decode of its event mask */
       const int32_t block_pos = pos;
@@ -93,7 +97,7 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
           m &= m - 1;
           uint32_t lo, hi;
           if (dec_event(d, (uint32_t) (block_pos + 64 * w) + bit, maxh, lo, hi)) {
-            rhp_hdr_t &o = hout[d.nh - 1];
+            rhp_hdr_t &o = hout[(uint64_t) (d.nh - 1) * hs_hdr];
             o.name_off = (uint16_t) lo;
             o.name_len = (uint16_t) (lo >> 16);
             o.value_off = (uint16_t) hi;
@@ -118,7 +122,7 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
         r.num_headers = (uint16_t) d.nh;
         r.flags = 0;
         b->reqs[i] = r;
-        if (b->mode == RHP_MODE_HTTP) http_frame(b->bytes_rw + off, len, r, hout, &b->http[i]);
+        if (b->mode == RHP_MODE_HTTP) http_frame(b->bytes_rw + off, len, r, hout, hs_hdr, &b->http[i]);
       } else if (bad) {
         st_count.fast_bad++;
         rhp_req_t r;

@@ -59,7 +59,8 @@ struct PlainBytes {
  *           the buffer and size_t lengths, no limit (picohttpparser.h:51-52). */
 struct OutRec {
   rhp_req_t *r;
-  rhp_hdr_t *h;
+  rhp_hdr_t *h;        /* record k at h[k * hs] (the batch's header-major layout: hs = n) */
+  uint64_t hs;
   RHP_HDM void begin()
   {
     r->method_off = 0; r->method_len = 0; r->path_off = 0; r->path_len = 0;
@@ -68,10 +69,11 @@ struct OutRec {
   RHP_HDM int fail(int code) { r->ret = code; return code; }
   RHP_HDM void header(uint32_t n, bool fold, uint64_t name, uint64_t name_len, uint64_t vs, uint64_t vlen)
   {
-    h[n].name_off = fold ? (uint16_t) RHP_NAME_NULL : (uint16_t) name;
-    h[n].name_len = (uint16_t) name_len;
-    h[n].value_off = (uint16_t) vs;
-    h[n].value_len = (uint16_t) vlen;
+    rhp_hdr_t &o = h[n * hs];
+    o.name_off = fold ? (uint16_t) RHP_NAME_NULL : (uint16_t) name;
+    o.name_len = (uint16_t) name_len;
+    o.value_off = (uint16_t) vs;
+    o.value_len = (uint16_t) vlen;
   }
   RHP_HDM int done(uint64_t p, const uint64_t (&tok)[2][2], int minor, uint32_t n)
   {
@@ -173,16 +175,16 @@ RHP_HD int scalar_phr_t(Bytes &B, uint64_t len, uint32_t max, Out &out)
 }
 
 template <class Bytes>
-RHP_HD int scalar_phr_t(Bytes &B, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h)
+RHP_HD int scalar_phr_t(Bytes &B, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, uint64_t hs)
 {
-  OutRec o{r, h};
+  OutRec o{r, h, hs};
   return scalar_phr_t(B, len, max, o);
 }
 
-RHP_HD int scalar_phr(const uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h)
+RHP_HD int scalar_phr(const uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, uint64_t hs)
 {
   PlainBytes B{b};
-  return scalar_phr_t(B, len, max, r, h);
+  return scalar_phr_t(B, len, max, r, h, hs);
 }
 
 /* is_complete (picohttpparser.c:197-223), the slowloris pre-check that
@@ -219,11 +221,12 @@ RHP_HD uint32_t upper(uint32_t c) { return (c - 'a' < 26u) ? c - 32u : c; }
 struct HdrsRec {
   const uint8_t *b;
   const rhp_hdr_t *h;
-  RHP_HDM bool null(uint32_t i) const { return h[i].name_off == RHP_NAME_NULL; }
-  RHP_HDM const uint8_t *name(uint32_t i) const { return b + h[i].name_off; }
-  RHP_HDM uint64_t name_len(uint32_t i) const { return h[i].name_len; }
-  RHP_HDM const uint8_t *value(uint32_t i) const { return b + h[i].value_off; }
-  RHP_HDM uint64_t value_len(uint32_t i) const { return h[i].value_len; }
+  uint64_t hs;         /* record i at h[i * hs] */
+  RHP_HDM bool null(uint32_t i) const { return h[i * hs].name_off == RHP_NAME_NULL; }
+  RHP_HDM const uint8_t *name(uint32_t i) const { return b + h[i * hs].name_off; }
+  RHP_HDM uint64_t name_len(uint32_t i) const { return h[i * hs].name_len; }
+  RHP_HDM const uint8_t *value(uint32_t i) const { return b + h[i * hs].value_off; }
+  RHP_HDM uint64_t value_len(uint32_t i) const { return h[i * hs].value_len; }
 };
 
 /* Case-insensitive name compare.  All n bytes are read before any is tested
@@ -397,11 +400,11 @@ RHP_HD void http_frame_t(uint8_t *b, uint64_t len, int64_t n, bool get, const HV
   }
 }
 
-RHP_HD void http_frame(uint8_t *b, uint64_t len, const rhp_req_t &r, const rhp_hdr_t *h, rhp_http_t *x,
+RHP_HD void http_frame(uint8_t *b, uint64_t len, const rhp_req_t &r, const rhp_hdr_t *h, uint64_t hs, rhp_http_t *x,
                        uint64_t cand = ~0ull)
 {
   const bool get = r.method_len == 3 && ((b[r.method_off] == 'G') & (b[r.method_off + 1] == 'E') & (b[r.method_off + 2] == 'T'));
-  http_frame_t(b, len, r.ret, get, HdrsRec{b, h}, r.num_headers, x, cand);
+  http_frame_t(b, len, r.ret, get, HdrsRec{b, h, hs}, r.num_headers, x, cand);
 }
 
 /* phr status -> http_read_request result when the parse gave no request
@@ -411,18 +414,19 @@ RHP_HD int32_t http_result_of(int n) { return n == kBad ? -1 : n == RHP_RET_TOOL
 
 /* Whole http_read_request for one request. */
 template <class Bytes>
-RHP_HD void scalar_http_t(Bytes &B, uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, rhp_http_t *x)
+RHP_HD void scalar_http_t(Bytes &B, uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, uint64_t hs,
+                          rhp_http_t *x)
 {
-  int n = scalar_phr_t(B, len, max, r, h);
+  int n = scalar_phr_t(B, len, max, r, h, hs);
   x->body_kind = 0; x->consumed = 0; x->body_len = 0;
   if (len == 0) { x->result = 0; return; }
   if (n <= 0) { x->result = http_result_of(n); return; }
-  http_frame(b, len, *r, h, x);
+  http_frame(b, len, *r, h, hs, x);
 }
-RHP_HD void scalar_http(uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, rhp_http_t *x)
+RHP_HD void scalar_http(uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, uint64_t hs, rhp_http_t *x)
 {
   PlainBytes B{b};
-  scalar_http_t(B, b, len, max, r, h, x);
+  scalar_http_t(B, b, len, max, r, h, hs, x);
 }
 
 }  // namespace rhp

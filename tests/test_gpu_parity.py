@@ -27,11 +27,12 @@ def golden(name):
     return spec, buf, off, (z["reqs"], z["hdrs"], z["http"] if "http" in z.files else None), z
 
 
-@pytest.mark.parametrize("impl", [rhp.IMPL_DFA, rhp.IMPL_EXACT])
+@pytest.mark.parametrize("impl,layout", [(rhp.IMPL_DFA, rhp.LAYOUT_REQUEST_MAJOR), (rhp.IMPL_EXACT, rhp.LAYOUT_REQUEST_MAJOR),
+                                         (rhp.IMPL_DFA, rhp.LAYOUT_HEADER_MAJOR), (rhp.IMPL_EXACT, rhp.LAYOUT_HEADER_MAJOR)])
 @pytest.mark.parametrize("name", sorted(MANIFEST))
-def test_gpu_matches_reference_golden(name, impl):
+def test_gpu_matches_reference_golden(name, impl, layout):
     spec, buf, off, want, z = golden(name)
-    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], impl=impl)
+    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], impl=impl, layout=layout)
     assert_same(canon(res, spec["mode"]), want, buf, off, f"GPU impl{impl} vs golden {name}")
     if "bytes_out_sha256" in z.files:
         assert hashlib.sha256(res.bytes_out.tobytes()).digest() == z["bytes_out_sha256"].tobytes()
@@ -166,7 +167,8 @@ def test_gpu_full_size_matches_reference_digest(name):
     the compiled reference's (tests/golden/full_digests.json)."""
     spec = FULL[name]
     buf, off = inputs(spec)
-    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"])
+    layout = rhp.LAYOUT_HEADER_MAJOR if "shard" in name else rhp.LAYOUT_REQUEST_MAJOR
+    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], layout=layout)
     got = canon(res, spec["mode"])
     if record_digest(*got) != spec["records_sha256"]:   # say which request differs
         want = to_rhp(*run_oracle(buf, off, spec["max_headers"], spec["mode"])[:3], spec["mode"])

@@ -35,10 +35,11 @@ def test_oracle_matches_reference_golden(name):
         assert hashlib.sha256(out.tobytes()).digest() == z["bytes_out_sha256"].tobytes()
 
 
+@pytest.mark.parametrize("layout", [rhp.LAYOUT_REQUEST_MAJOR, rhp.LAYOUT_HEADER_MAJOR])
 @pytest.mark.parametrize("name", sorted(SETS))
-def test_dfa_emulation_matches_golden(name):
+def test_dfa_emulation_matches_golden(name, layout):
     spec, buf, off, want, z = load_golden(name)
-    res, stats = rhp.emulate(buf, off, spec["max_headers"], spec["mode"])
+    res, stats = rhp.emulate(buf, off, spec["max_headers"], spec["mode"], layout)
     assert_same(canon(res, spec["mode"]), want, buf, off, f"DFA emulation vs golden {name}")
     if "bytes_out_sha256" in z.files:
         assert hashlib.sha256(res.bytes_out.tobytes()).digest() == z["bytes_out_sha256"].tobytes()
@@ -47,7 +48,7 @@ def test_dfa_emulation_matches_golden(name):
 @pytest.mark.parametrize("name", sorted(SETS))
 def test_cpu_exact_parser_matches_golden(name):
     spec, buf, off, want, z = load_golden(name)
-    res = rhp.parse_cpu_exact(buf, off, spec["max_headers"], spec["mode"])
+    res = rhp.parse_cpu_exact(buf, off, spec["max_headers"], spec["mode"], rhp.LAYOUT_HEADER_MAJOR)
     assert_same(canon(res, spec["mode"]), want, buf, off, f"CPU exact parser vs golden {name}")
 
 

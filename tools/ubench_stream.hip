@@ -149,6 +149,49 @@ __global__ void dma(const uint8_t *buf, uint64_t bytes, uint32_t *out)
   clk_end(t, r);
 }
 
+// record writes: each lane owns a 128-B line (a request's max_headers = 16
+// record slots) and writes the first BYTES of it with STORE-byte stores
+template <int BYTES, int STORE>
+__global__ void wrec(uint8_t *dst, uint64_t lines, uint32_t *out)
+{
+  const uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= lines) return;
+  uint8_t *l = dst + i * 128;
+  if (STORE == 16) {
+#pragma unroll
+    for (int q = 0; q < BYTES / 16; q++)
+      *reinterpret_cast<__attribute__((address_space(1))) u32x4 *>((uintptr_t) (l + 16 * q)) = u32x4{(uint32_t) i, 1, 2, 3};
+  } else {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int q = 0; q < BYTES / 8; q++)
+      *reinterpret_cast<__attribute__((address_space(1))) u32x2 *>((uintptr_t) (l + 8 * q)) = u32x2{(uint32_t) i, 1};
+  }
+}
+
+template <class F>
+void run_w(const char *name, F fn, uint8_t *dst, uint64_t lines, uint32_t *out)
+{
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  const int block = 256;
+  const int grid = (int) ((lines + block - 1) / block);
+  float best = 1e9;
+  for (int rep = 0; rep < 6; rep++) {
+    CHECK(hipMemset(dst, 0, lines * 128));
+    CHECK(hipEventRecord(a));
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(block), 0, 0, dst, lines, out);
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    if (rep && ms < best) best = ms;
+  }
+  printf("%-34s %8.1f us for %llu lines\n", name, best * 1e3, (unsigned long long) lines);
+  fflush(stdout);
+}
+
 template <class F>
 void run(const char *name, F fn, int grid, int block, size_t lds, const uint8_t *buf, uint64_t bytes, uint32_t *out)
 {
@@ -189,6 +232,16 @@ int main(int argc, char **argv)
   CHECK(hipMalloc(&buf, bytes + 65536));
   CHECK(hipMemset(buf, 0x41, bytes + 65536));
   CHECK(hipMalloc(&out, 64u << 20));
+  if (only[0] == 'w') {   /* record-write patterns, 1M lines (config 2's hdrs array) */
+    const uint64_t lines = 1u << 20;
+    uint8_t *dst = buf + (1ull << 30);
+    run_w("write 32 B of 128 (2 x 16 B)", wrec<32, 16>, dst, lines, out);
+    run_w("write 32 B of 128 (4 x 8 B)", wrec<32, 8>, dst, lines, out);
+    run_w("write 64 B of 128 (4 x 16 B)", wrec<64, 16>, dst, lines, out);
+    run_w("write 128 B of 128 (8 x 16 B)", wrec<128, 16>, dst, lines, out);
+    run_w("write 16 B of 128 (1 x 16 B)", wrec<16, 16>, dst, lines, out);
+    return 0;
+  }
   if (only[0]) {
     /* FETCH_SIZE calibration: 2 GiB read by whole-line LDS-DMA windows, then by
      * the same windows 36 B off line alignment (every window straddles two lines) */

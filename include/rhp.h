@@ -105,7 +105,8 @@ typedef struct rhp_batch {
   uint32_t        mode;        /* enum rhp_mode */
   uint32_t        layout;      /* enum rhp_layout: where record k of request i lives in hdrs */
   rhp_req_t      *reqs;        /* device [n] */
-  rhp_hdr_t      *hdrs;        /* device [n * max_headers] records, laid out as `layout` says */
+  rhp_hdr_t      *hdrs;        /* device [n * max_headers] records, laid out as `layout` says
+                                  (n * max_headers < 2^32) */
   rhp_http_t     *http;        /* device [n], RHP_MODE_HTTP */
   uint32_t       *work;        /* reserved, may be NULL (device scratch of RHP_WORK_WORDS u32
                                   for future kernels; the current ones keep their scheduling

@@ -11,15 +11,16 @@
  *        code   = T[r * 256 + b0]                    ds_read_u8 (independent)
  *        idx    = T[v_perm(idx, code)]               one dependent ds_read_u8
  *        ev     = v_alignbit(idx, ev, 2)             low index bits = event bits
- *  - lanes stream their request in 128-byte windows = whole HBM lines: the
- *    wave fetches its 64 lanes' next windows with eight LDS-DMA loads (8
- *    lines each) one block ahead of use; every lane also holds its NEXT
- *    request's offsets, so a request switch never waits on a dependent load;
- *  - the events of a window are decoded into records while the NEXT window is
- *    walked: the walk is a chain of dependent LDS reads whose latency leaves
- *    the issue slots free, and the decode -- branch-free event slots, one
- *    event per slot -- fills them (a decode that ran between two walks cost
- *    45 % of the kernel's time, profiles/r02/b/kclock_variants.txt);
+ *  - lanes stream their request in 128-byte windows (4-aligned): the wave
+ *    fetches its 64 lanes' next windows with eight LDS-DMA loads (8 windows
+ *    each) one iteration ahead of use, and every lane holds its NEXT request's
+ *    offsets, so neither a window nor a request switch waits on a dependent
+ *    load (lane-per-window loads straight into registers, interleaved with the
+ *    walk, took 43 % longer: profiles/r02/c/ab_direct.txt);
+ *  - the events of a window are decoded into records (prefix-XOR split of the
+ *    alternating colon / line-end events, one loop trip per header) one
+ *    iteration behind the walk, into the issue slots its dependent LDS reads
+ *    leave free;
  *  - a request the table cannot decide alone (S_SLOW, a terminal at/after
  *    len, no terminal by the end of its buffer) and http framing are finished
  *    after the loop by the workgroup's replay (rhp_scalar.h exact path through
@@ -99,6 +100,7 @@ __device__ __forceinline__ uint32_t dma_part(uint32_t w, uint32_t j) { return ((
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 #ifdef RHP_STAMPS
 /* diagnostic build only: per-wave shader-cycle sums per loop section, stored by
@@ -461,61 +463,99 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   };
 
   /* ---- decode ----
-   * The decoded window's events as two 64-bit halves (mh0: bytes 0..63, mh1:
-   * 64..127 of the window at dpos), the terminal taken off.  The grammar fixes
-   * their order (rhp_dfa.h): ME PE RL, then per header line its colon (CO) and
-   * its LF (EOL).  The request-line events go through up to three slots; in
-   * the header region the events alternate, so a prefix XOR of a half splits
-   * it into its CO and EOL bits and one loop iteration completes one record:
+   * The decoded window's events as four 32-bit words mq[q] (bytes 32q..32q+31
+   * of the window at dpos), the terminal taken off.  The grammar fixes their
+   * order (rhp_dfa.h): ME PE RL, then per header line its colon (CO) and its LF
+   * (EOL).  Per word, the request-line events of lanes still in the request
+   * line go through a small loop; in the header region the events alternate,
+   * so a prefix XOR splits the word into its CO and EOL bits and one loop
+   * iteration completes one record:
    *   name = [ls, co), value = [co + 2, eol - 1), next ls = eol + 1.
    * The max_headers check (picohttpparser.c:281-284) fires at the CO of a line
-   * that starts while nh == maxh; decoding stops there (masks cleared), so nh
-   * never exceeds maxh and every completed record is stored. */
-  uint64_t mh0 = 0, mh1 = 0;
-  uint32_t term_pos = 0xffffffffu;
-  auto rl_slot = [&]() {   /* the lowest event, for lanes still in the request line */
-    const bool lo = mh0 != 0;
-    const uint64_t m = lo ? mh0 : mh1;
-    const bool v = m != 0 && (kn & 7u) < 3u;
-    const uint32_t ep = (uint32_t) dpos + (lo ? 0u : 64u) + (uint32_t) __builtin_ctzll(m | (1ull << 63));
-    const uint64_t rest = v ? m & (m - 1u) : m;
-    mh0 = lo ? rest : mh0;
-    mh1 = lo ? mh1 : rest;
-    const uint32_t k = v ? kn & 7u : 7u;
-    /* ME: method_len = ME (the DFA path parses the method from byte 0);
-     * PE: path = [ME + 1, PE), the first header line starts at PE + 11;
-     * RL: at the CR of "HTTP/1.0" (PE + 9) or the LF of "HTTP/1.1" (PE + 10) */
-    uint32_t lsn = ep + 11u, rln = me | ((ep - me - 1u) << 16), mv = ((ep - pe - 9u) & 1u) << 3;
-    opaque(lsn); opaque(rln); opaque(mv);
-    me = k == 0u ? ep : me;
-    pe = k == 1u ? ep : pe;
-    rl = k == 1u ? rln : rl;
-    ls = k == 1u ? lsn : ls;
-    kn += k == 2u ? 1u + mv : k < 2u ? 1u : 0u;
-  };
-  rhp_hdr_t *hout = p.hdrs;
-  auto headers_half = [&](uint64_t m, uint32_t base) {
+   * that starts while nh == maxh; decoding stops there (dstop), so nh never
+   * exceeds maxh and every completed record is stored.  Updates are written as
+   * arithmetic on the conditions (m & (m - c), x + c * d) so the compiler emits
+   * straight-line code, not exec-masked branches. */
+  uint32_t mq[kEvWords];
+  uint32_t term_pos = 0xffffffffu, dstop = 0;
+  /* hx: index in hdrs of the decoded request's next header record (set per
+   * window from dcur and nh, not carried across the walk; the host keeps
+   * n * max_headers below 2^32) */
+  uint32_t hx = 0;
+  auto word = [&](uint32_t m, uint32_t base) {
+    m &= dstop - 1u;   /* nothing after a max_headers stop */
+    if (!__builtin_amdgcn_ballot_w64(m != 0)) return;
+    /* request line: ME -> method_len = ME (the DFA path parses the method from
+     * byte 0); PE -> path = [ME + 1, PE), the first header line starts at
+     * PE + 11; RL at the CR of "HTTP/1.0" (PE + 9) or the LF of "HTTP/1.1" */
+    while (__builtin_amdgcn_ballot_w64(m != 0 && (kn & 7u) < 3u)) {
+      const uint32_t v = m != 0 && (kn & 7u) < 3u;
+      const uint32_t ep = base + (uint32_t) __builtin_ctz(m | 0x80000000u);
+      m &= m - v;
+      const uint32_t k = v ? kn & 7u : 7u;
+      const uint32_t mv = ((ep - pe - 9u) & 1u) << 3;
+      rl = k == 1u ? me | ((ep - me - 1u) << 16) : rl;
+      ls = k == 1u ? ep + 11u : ls;
+      me = k == 0u ? ep : me;
+      pe = k == 1u ? ep : pe;
+      kn += (k < 3u) + (k == 2u ? mv : 0u);
+    }
     if (!__builtin_amdgcn_ballot_w64(m != 0)) return;
     /* prefix XOR: bit i = parity of the events at or below i, 1 at the 1st,
-     * 3rd, ... event of the half */
-    uint64_t px = m;
-    px ^= px << 1; px ^= px << 2; px ^= px << 4; px ^= px << 8; px ^= px << 16; px ^= px << 32;
-    const uint64_t odd = m & px, even = m & ~px;
-    uint64_t com = t ? even : odd, eolm = t ? odd : even;   /* t = 1: the half opens with an EOL */
+     * 3rd, ... event of the word */
+    uint32_t px = m ^ (m << 1);
+    px ^= px << 2; px ^= px << 4; px ^= px << 8; px ^= px << 16;
+    const uint32_t odd = m & px;
+    uint32_t com = t ? m ^ odd : odd;    /* t = 1: the word opens with an EOL */
+    uint32_t eolm = m ^ com;
+    if (!__builtin_amdgcn_ballot_w64(nh + (uint32_t) __builtin_popcount(eolm) >= maxh)) {
+      /* no lane can reach max_headers in this word: no capacity checks */
+      /* Straight-line body for every lane (a masked `if` costs more in copies
+       * than it saves): a lane whose word is done (eolm == 0) computes a dead
+       * record, stores nothing and keeps its state */
+      while (uint64_t st_m = __builtin_amdgcn_ballot_w64(eolm != 0)) {
+        const bool has = eolm != 0;
+        const uint32_t e = base + (uint32_t) __builtin_ctz(eolm | 0x80000000u);
+        const uint32_t co = t ? pco : base + (uint32_t) __builtin_ctz(com | 0x80000000u);
+        const uint32_t lo = ls | ((co - ls) << 16), hi = (co + 2u) | ((e - co - 3u) << 16);
+#ifndef RHP_EXP_NOSTORE   /* timing experiment: header records computed, not stored */
+        store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi});
+#endif
+        if (http) {   /* uniform: framing candidates only in http mode */
+          const uint32_t nlen = co - ls;
+          const bool cnd = has && (nlen == 14u || nlen == 17u);
+          const bool first = cnd && (cand & 0xbfffffffu) == 0;
+          crec_lo = first ? lo : crec_lo;
+          crec_hi = first ? hi : crec_hi;
+          cand |= cnd ? (nh < 30u ? 1u << nh : 0x80000000u) : 0u;
+        }
+        com &= com - (uint32_t) (has && !t);
+        eolm &= eolm - 1u;
+        ls = has ? e + 1u : ls;
+        nh += (uint32_t) has;
+        hx += has ? p.hs_hdr : 0u;
+        t = has ? 0u : t;
+      }
+      /* a colon left open at the end of the word: a later word (or window) has its LF */
+      if (com) {
+        pco = base + (uint32_t) __builtin_ctz(com);
+        t = 1;
+      }
+      return;
+    }
     while (__builtin_amdgcn_ballot_w64(eolm != 0)) {
       const bool has = eolm != 0;
-      const uint32_t e = base + (uint32_t) __builtin_ctzll(eolm | (1ull << 63));
-      const uint32_t cm = base + (uint32_t) __builtin_ctzll(com | (1ull << 63));
-      const bool newline = has && !t;           /* this record's CO is in the mask */
-      const bool stop = newline && nh == maxh;  /* a line starts at capacity: -1 (or exact) */
+      const uint32_t e = base + (uint32_t) __builtin_ctz(eolm | 0x80000000u);
+      const uint32_t co = t ? pco : base + (uint32_t) __builtin_ctz(com | 0x80000000u);
+      const bool nl = has && !t;                   /* this record's CO is in the word */
+      const bool stop = nl && nh == maxh;          /* a line starts at capacity: -1 (or exact) */
       const bool rec = has && !stop;
-      const uint32_t co = t ? pco : cm;
       const uint32_t lo = ls | ((co - ls) << 16), hi = (co + 2u) | ((e - co - 3u) << 16);
       const uint64_t st_m = __builtin_amdgcn_ballot_w64(rec);
-#ifndef RHP_EXP_NOSTORE   /* timing experiment: header records computed, not stored */
-      if (st_m) store_rec_lanes(st_m, hout + (uint64_t) nh * p.hs_hdr, u32x2{lo, hi});
+#ifndef RHP_EXP_NOSTORE
+      if (st_m) store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi});
 #endif
-      if (http) {   /* uniform: framing candidates only in http mode */
+      if (http) {
         const uint32_t nlen = co - ls;
         const bool cnd = rec && (nlen == 14u || nlen == 17u);
         const bool first = cnd && (cand & 0xbfffffffu) == 0;
@@ -523,60 +563,46 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         crec_hi = first ? hi : crec_hi;
         cand |= cnd ? (nh < 30u ? 1u << nh : 0x80000000u) : 0u;
       }
-      uint32_t ovn = ls + 1u, lsn = e + 1u;
-      opaque(ovn); opaque(lsn);
-      ovf = stop && ovf == 0 ? ovn : ovf;
-      com = newline && !stop ? com & (com - 1u) : stop ? 0 : com;
-      eolm = rec ? eolm & (eolm - 1u) : stop ? 0 : eolm;
+      ovf = stop && ovf == 0 ? ls + 1u : ovf;
+      dstop |= stop ? 1u : 0u;
+      com = stop ? 0u : nl ? com & (com - 1u) : com;
+      eolm = stop ? 0u : rec ? eolm & (eolm - 1u) : eolm;
+      ls = rec ? e + 1u : ls;
       nh += rec ? 1u : 0u;
-      ls = rec ? lsn : ls;
+      hx += rec ? p.hs_hdr : 0u;
       t = rec ? 0u : t;
-      if (stop) { mh0 = 0; mh1 = 0; }
     }
-    /* a colon left open at the end of the half: the next half (or window) has its LF */
     const bool open = com != 0;
     const bool stop = open && nh == maxh;
-    uint32_t ovn = ls + 1u;
-    opaque(ovn);
-    ovf = stop && ovf == 0 ? ovn : ovf;
-    pco = open && !stop ? base + (uint32_t) __builtin_ctzll(com) : pco;
+    ovf = stop && ovf == 0 ? ls + 1u : ovf;
+    dstop |= stop ? 1u : 0u;
+    pco = open && !stop ? base + (uint32_t) __builtin_ctz(com) : pco;
     t = open && !stop ? 1u : t;
-    if (stop) { mh0 = 0; mh1 = 0; }
   };
   auto decode_window = [&]() {
-    if (__builtin_amdgcn_ballot_w64((kn & 7u) < 3u && (mh0 | mh1) != 0)) {
-      rl_slot();
-      rl_slot();
-      rl_slot();
-    }
-    /* events before RL never reach the header loop: lanes still in the
-     * request line have none left here */
-    headers_half(mh0, (uint32_t) dpos);
-    headers_half(mh1, (uint32_t) dpos + 64u);
-    mh0 = mh1 = 0;
+#pragma unroll
+    for (int q = 0; q < (int) kEvWords; q++) word(mq[q], (uint32_t) dpos + 32u * (uint32_t) q);
   };
   /* set up the decode of the window walked last iteration */
   auto decode_begin = [&]() {
     const uint32_t e = st_prev;
     const bool slow = is_slow2(e);
     const bool term_ev = is_done2(e) || is_err2(e);
-    uint64_t h0 = ((uint64_t) evp[1] << 32) | evp[0], h1 = ((uint64_t) evp[3] << 32) | evp[2];
-    if (slow || !dhas || ovf) h0 = h1 = 0;
+    const uint32_t live = (slow || !dhas || ovf) ? 0u : 0xffffffffu;
+#pragma unroll
+    for (int q = 0; q < (int) kEvWords; q++) mq[q] = evp[q] & live;
     term_pos = 0xffffffffu;
+    dstop = 0;
+    hx = dcur * p.hs_req + nh * p.hs_hdr;
     if (term_ev) {   /* the terminal is the window's last event: take it off the mask */
-      if (h1) {
-        const uint32_t bt = 63u - (uint32_t) __builtin_clzll(h1);
-        term_pos = (uint32_t) dpos + 64u + bt;
-        h1 &= ~(1ull << bt);
-      } else if (h0) {
-        const uint32_t bt = 63u - (uint32_t) __builtin_clzll(h0);
-        term_pos = (uint32_t) dpos + bt;
-        h0 &= ~(1ull << bt);
-      }
+      const int q = mq[3] ? 3 : mq[2] ? 2 : mq[1] ? 1 : 0;
+      uint32_t w = q == 3 ? mq[3] : q == 2 ? mq[2] : q == 1 ? mq[1] : mq[0];
+      const uint32_t bt = 31u - (uint32_t) __builtin_clz(w | 1u);
+      if (w) term_pos = (uint32_t) dpos + 32u * (uint32_t) q + bt;
+      w &= ~(1u << bt);
+#pragma unroll
+      for (int k = 0; k < (int) kEvWords; k++) mq[k] = k == q ? w : mq[k];
     }
-    mh0 = h0;
-    mh1 = h1;
-    hout = p.hdrs + (uint64_t) dcur * p.hs_req;
   };
   /*
    * Finalize dcur when its outcome is known (decisions mirrored by rhp_emu.cpp):
@@ -684,14 +710,15 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
      * windows, which then hit in L2 (non-temporal: config 3 -5 %) */
     const bool aligned = !(nw & 3u) || ((uint32_t) (uintptr_t) (wbytes + src) & (kBlock - 1u)) == 0;
     const bool nt = !__builtin_amdgcn_ballot_w64(!aligned);
-#pragma unroll
-    for (int i = 0; i < (int) kParts; i++) {
-      const uint32_t part = dma_part(dma_window((uint32_t) i, lane), lane);
-      const void *g = reinterpret_cast<const void *>(wbytes + a[i] + 16u * part);
-      __attribute__((address_space(3))) void *l = (__attribute__((address_space(3))) void *) (lds + stage + 1024u * i);
-      if (nt) __builtin_amdgcn_global_load_lds(g, l, 16, 0, 2);
-      else __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
+    /* one branch per issue, not one per load (the cache policy is an immediate) */
+#define RHP_ISSUE_LOADS(AUX)                                                                             \
+    _Pragma("unroll") for (int i = 0; i < (int) kParts; i++) {                                           \
+      const uint32_t part = dma_part(dma_window((uint32_t) i, lane), lane);                              \
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(wbytes + a[i] + 16u * part),       \
+          (__attribute__((address_space(3))) void *) (lds + stage + 1024u * i), 16, 0, AUX);             \
     }
+    if (nt) { RHP_ISSUE_LOADS(2) } else { RHP_ISSUE_LOADS(0) }
+#undef RHP_ISSUE_LOADS
   };
 
   refill_pend();
@@ -708,8 +735,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * One iteration = one 128-byte window per lane.
    * [A] the window issued one iteration earlier has landed (the loop's only
    * VMEM wait) -> [C] switch the walk to it -> [D] hand out pending requests
-   * -> [E] issue the next window into the buffer [A] just read -> [F] walk
-   * the window, decoding the previous one in its shadow -> [G] finalize the
+   * -> [E] issue the next window into the buffer [A] just read -> decode the
+   * previous window -> [F] walk this one -> [G] finalize the
    * decoded request if it ended, hand the decode over to the walked window.
    */
 #ifdef RHP_STAMPS
@@ -965,6 +992,7 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   if (((uintptr_t) b->bytes & 15u) != 0) return -22;   /* windows and exact-path lines are aligned loads */
   if (b->max_headers > RHP_MAX_HEADERS) return -22;
   if (b->max_headers > 0 && !b->hdrs) return -22;
+  if ((uint64_t) b->n * b->max_headers > 0xffffffffull) return -22;   /* record indices are 32-bit */
   if (b->mode == RHP_MODE_HTTP && (!b->http || !b->bytes_rw)) return -22;
   if (b->mode != RHP_MODE_PHR && b->mode != RHP_MODE_HTTP) return -22;
   if (b->layout != RHP_LAYOUT_REQUEST_MAJOR && b->layout != RHP_LAYOUT_HEADER_MAJOR) return -22;

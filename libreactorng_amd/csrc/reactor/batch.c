@@ -3,18 +3,31 @@
  * (include/rhp.h) over the packed unconsumed input of every session that has
  * bytes to parse in a reactor round.
  *
- * "gpu" (default): pinned host staging -> hipMemcpyAsync H2D -> the MI355X
- * kernel -> D2H of the records, on one HIP stream of this thread.  The parser
- * is the product path: when RHP_REACTOR_PARSER is unset or "gpu" and no GPU or
- * librhp.so is usable, the process stops with an error (no silent fallback).
+ * "gpu" (default): a round is packed into one of REACTOR_BATCH_SLOTS pinned
+ * host slots, then H2D copies, the MI355X kernel and the D2H copies of the
+ * records are queued on this thread's HIP stream and the call returns.  A host
+ * function queued behind them writes the thread's eventfd, which the server
+ * polls from the reactor loop (the reference's reactor_async pattern,
+ * reactor.c:316-330: work off the loop, completion by eventfd), so the loop
+ * keeps serving sockets, and the server packs the next round, while a round
+ * parses.  The parser is the product path: when RHP_REACTOR_PARSER is unset or
+ * "gpu" and no GPU or librhp.so is usable, the process stops with an error (no
+ * silent fallback).
  * "host": the product's exact scalar parser (rhp_cpu_parse_batch) in place,
- * selected explicitly for CPU-only hosts and the CPU test suite.
+ * synchronously, selected explicitly for CPU-only hosts and the CPU suite.
+ * "host-async": the same parser on a worker thread with the gpu mode's
+ * completion protocol (slots, eventfd), so the CPU suite exercises the
+ * server's pipelined rounds.
  */
 #define __HIP_PLATFORM_AMD__ 1
+#include <errno.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
+#include <sys/eventfd.h>
 #include <hip/hip_runtime_api.h>
 
 #include "reactor.h"
@@ -22,24 +35,66 @@
 #include "rhp.h"
 #include "rhp_host.h"
 
-enum { PARSER_UNSET, PARSER_GPU, PARSER_HOST };
+enum { PARSER_UNSET, PARSER_GPU, PARSER_HOST, PARSER_HOST_ASYNC };
 
-static __thread struct
+typedef struct slot
 {
-  int          parser;
-  size_t       cap_bytes, cap_n, cap_h;
+  size_t       cap_bytes, cap_n;
   uint8_t     *h_bytes;      /* pinned (gpu) or malloc'd (host) staging */
   uint64_t    *h_off;
   rhp_req_t   *h_req;
   rhp_hdr_t   *h_hdr;
   rhp_http_t  *h_http;
-  void        *d_bytes, *d_off, *d_req, *d_hdr, *d_http, *d_work;
+  void        *d_bytes, *d_off, *d_req, *d_hdr, *d_http;
+  uint32_t     n;
+  size_t       bytes;
+  uint64_t     t_submit;
+} slot_t;
+
+typedef struct batch_state
+{
+  int          parser;
   hipStream_t  stream;
-  /* RHP_REACTOR_STATS=1: rounds, requests and time spent in the parser, printed at exit */
+  int          efd;          /* gpu: written once per completed round */
+  slot_t       slot[REACTOR_BATCH_SLOTS];
+  void        *d_work;
+  /* RHP_REACTOR_STATS=1: rounds, requests and submit -> result time, printed at exit */
   int          stats;
   int          diag_host;   /* RHP_REACTOR_DIAG=hostparse: gpu-mode buffers, host parse (diagnostic) */
   uint64_t     st_rounds, st_requests, st_ns;
-} B;
+  /* host-async: the worker's queue of submitted slots (in order) */
+  pthread_t       worker;
+  pthread_mutex_t mu;
+  pthread_cond_t  cv;
+  int             q[REACTOR_BATCH_SLOTS], q_head, q_n;
+} batch_state_t;
+
+static __thread batch_state_t B;   /* one parser per reactor thread */
+
+static void host_parse(batch_state_t *b, int k);
+
+/* host-async worker: the state is its creator's (B is per thread) */
+static void *host_worker(void *arg)
+{
+  batch_state_t *b = arg;
+  pthread_mutex_lock(&b->mu);
+  for (;;)
+  {
+    while (!b->q_n)
+      pthread_cond_wait(&b->cv, &b->mu);
+    const int k = b->q[b->q_head];
+    pthread_mutex_unlock(&b->mu);
+    host_parse(b, k);
+    const uint64_t one = 1;
+    ssize_t r = write(b->efd, &one, sizeof one);
+    (void) r;
+    pthread_mutex_lock(&b->mu);
+    b->q_head = (b->q_head + 1) % REACTOR_BATCH_SLOTS;
+    b->q_n--;
+    pthread_cond_broadcast(&b->cv);
+  }
+  return NULL;
+}
 
 static uint64_t now_ns(void)
 {
@@ -50,7 +105,7 @@ static uint64_t now_ns(void)
 
 static void print_stats(void)
 {
-  fprintf(stderr, "reactor parser %s: %llu rounds, %llu requests (%.1f per round), %.1f us per round\n",
+  fprintf(stderr, "reactor parser %s: %llu rounds, %llu requests (%.1f per round), %.1f us per round (submit to result)\n",
           B.parser == PARSER_GPU ? "gpu" : "host", (unsigned long long) B.st_rounds, (unsigned long long) B.st_requests,
           B.st_rounds ? (double) B.st_requests / (double) B.st_rounds : 0.0,
           B.st_rounds ? (double) B.st_ns / 1e3 / (double) B.st_rounds : 0.0);
@@ -70,12 +125,14 @@ static int parser(void)
   if (B.parser == PARSER_UNSET)
   {
     const char *e = getenv("RHP_REACTOR_PARSER");
-    B.parser = e && strcmp(e, "host") == 0 ? PARSER_HOST : PARSER_GPU;
+    B.parser = !e ? PARSER_GPU : strcmp(e, "host") == 0 ? PARSER_HOST : strcmp(e, "host-async") == 0 ? PARSER_HOST_ASYNC
+                                                                                                       : PARSER_GPU;
     const char *st = getenv("RHP_REACTOR_STATS");
     if ((B.stats = st && *st == '1'))
       atexit(print_stats);
     const char *dg = getenv("RHP_REACTOR_DIAG");
     B.diag_host = dg && strcmp(dg, "hostparse") == 0;
+    B.efd = -1;
     if (B.parser == PARSER_GPU)
     {
       int n = 0;
@@ -84,13 +141,39 @@ static int parser(void)
         die("hipGetDeviceCount", 0);
       HIP(hipStreamCreateWithFlags(&B.stream, hipStreamNonBlocking));
     }
+    if (B.parser != PARSER_HOST)
+    {
+      B.efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+      if (B.efd < 0)
+        die("eventfd", errno);
+    }
+    if (B.parser == PARSER_HOST_ASYNC)
+    {
+      pthread_mutex_init(&B.mu, NULL);
+      pthread_cond_init(&B.cv, NULL);
+      if (pthread_create(&B.worker, NULL, host_worker, &B) != 0)
+        abort();
+      pthread_detach(B.worker);
+    }
   }
   return B.parser;
 }
 
 const char *reactor_parser_name(void)
 {
-  return parser() == PARSER_GPU ? "gpu" : "host";
+  const int p = parser();
+  return p == PARSER_GPU ? "gpu" : p == PARSER_HOST_ASYNC ? "host-async" : "host";
+}
+
+int reactor_batch_async(void)
+{
+  return parser() != PARSER_HOST;
+}
+
+int reactor_batch_fd(void)
+{
+  (void) parser();
+  return B.efd;
 }
 
 static void *host_alloc(size_t n)
@@ -120,116 +203,171 @@ static void dev_free(void **p)
   *p = NULL;
 }
 
-uint8_t *reactor_batch_reserve(size_t bytes, uint32_t n)
+uint8_t *reactor_batch_reserve(int k, size_t bytes, uint32_t n)
 {
   (void) parser();
-  const uint64_t t0 = B.stats ? now_ns() : 0;
+  slot_t *s = &B.slot[k];
   const size_t need = bytes + RHP_PAD;
-  if (need > B.cap_bytes)
+  if (need > s->cap_bytes)
   {
     /* generous first capacities: growing pinned and device buffers costs
      * milliseconds per step (page pinning, frees that synchronise) */
-    size_t c = B.cap_bytes ? B.cap_bytes : 1u << 20;
+    size_t c = s->cap_bytes ? s->cap_bytes : 1u << 20;
     while (c < need)
       c *= 2;
-    host_free(B.h_bytes);
-    B.h_bytes = host_alloc(c);
+    host_free(s->h_bytes);
+    s->h_bytes = host_alloc(c);
     if (B.parser == PARSER_GPU)
     {
-      dev_free(&B.d_bytes);
-      HIP(hipMalloc(&B.d_bytes, c));
+      dev_free(&s->d_bytes);
+      HIP(hipMalloc(&s->d_bytes, c));
     }
-    B.cap_bytes = c;
+    s->cap_bytes = c;
   }
-  if (n + 1 > B.cap_n)
+  if (n + 1 > s->cap_n)
   {
-    size_t c = B.cap_n ? B.cap_n : 4096;
+    size_t c = s->cap_n ? s->cap_n : 4096;
     while (c < n + 1u)
       c *= 2;
-    host_free(B.h_off);
-    host_free(B.h_req);
-    host_free(B.h_hdr);
-    host_free(B.h_http);
-    B.h_off = host_alloc(c * sizeof *B.h_off);
-    B.h_req = host_alloc(c * sizeof *B.h_req);
-    B.h_hdr = host_alloc(c * REACTOR_BATCH_HEADERS * sizeof *B.h_hdr);
-    B.h_http = host_alloc(c * sizeof *B.h_http);
+    host_free(s->h_off);
+    host_free(s->h_req);
+    host_free(s->h_hdr);
+    host_free(s->h_http);
+    s->h_off = host_alloc(c * sizeof *s->h_off);
+    s->h_req = host_alloc(c * sizeof *s->h_req);
+    s->h_hdr = host_alloc(c * REACTOR_BATCH_HEADERS * sizeof *s->h_hdr);
+    s->h_http = host_alloc(c * sizeof *s->h_http);
     if (B.parser == PARSER_GPU)
     {
-      dev_free(&B.d_off);
-      dev_free(&B.d_req);
-      dev_free(&B.d_hdr);
-      dev_free(&B.d_http);
-      HIP(hipMalloc(&B.d_off, c * sizeof *B.h_off));
-      HIP(hipMalloc(&B.d_req, c * sizeof *B.h_req));
-      HIP(hipMalloc(&B.d_hdr, c * REACTOR_BATCH_HEADERS * sizeof *B.h_hdr));
-      HIP(hipMalloc(&B.d_http, c * sizeof *B.h_http));
+      dev_free(&s->d_off);
+      dev_free(&s->d_req);
+      dev_free(&s->d_hdr);
+      dev_free(&s->d_http);
+      HIP(hipMalloc(&s->d_off, c * sizeof *s->h_off));
+      HIP(hipMalloc(&s->d_req, c * sizeof *s->h_req));
+      HIP(hipMalloc(&s->d_hdr, c * REACTOR_BATCH_HEADERS * sizeof *s->h_hdr));
+      HIP(hipMalloc(&s->d_http, c * sizeof *s->h_http));
       if (!B.d_work)
       {
         HIP(hipMalloc(&B.d_work, RHP_WORK_WORDS * sizeof(uint32_t)));
         HIP(hipMemsetAsync(B.d_work, 0, RHP_WORK_WORDS * sizeof(uint32_t), B.stream));
       }
     }
-    B.cap_n = c;
+    s->cap_n = c;
   }
-  if (B.stats)
-    B.st_ns += now_ns() - t0;
-  return B.h_bytes;
+  return s->h_bytes;
 }
 
-uint64_t *reactor_batch_offsets(void)
+uint64_t *reactor_batch_offsets(int k)
 {
-  return B.h_off;
+  return B.slot[k].h_off;
 }
 
-int reactor_batch_run(uint32_t n, size_t bytes, reactor_batch_result_t *out)
+/* runs on a HIP runtime thread once the round's copies have landed: wake the
+ * reactor loop (write(2) on an eventfd; no HIP call here) */
+static void round_done(void *arg)
 {
-  const uint64_t t0 = B.stats ? now_ns() : 0;
-  memset(B.h_bytes + bytes, 0, RHP_PAD);
-  B.h_off[n] = bytes;
+  const uint64_t one = 1;
+  ssize_t r = write((int) (intptr_t) arg, &one, sizeof one);
+  (void) r;
+}
+
+static void host_parse(batch_state_t *st, int k)
+{
+  slot_t *s = &st->slot[k];
+  rhp_batch_t b = {
+    .bytes = s->h_bytes, .bytes_rw = s->h_bytes, .offsets = s->h_off, .bytes_size = s->bytes + RHP_PAD, .n = s->n,
+    .max_headers = REACTOR_BATCH_HEADERS, .mode = RHP_MODE_HTTP, .reqs = s->h_req, .hdrs = s->h_hdr, .http = s->h_http};
+  (void) rhp_cpu_parse_batch(&b);
+}
+
+void reactor_batch_submit(int k, uint32_t n, size_t bytes)
+{
+  slot_t *s = &B.slot[k];
+  s->n = n;
+  s->bytes = bytes;
+  s->t_submit = B.stats ? now_ns() : 0;
+  memset(s->h_bytes + bytes, 0, RHP_PAD);
+  s->h_off[n] = bytes;
+  if (B.parser == PARSER_HOST_ASYNC)
+  {
+    pthread_mutex_lock(&B.mu);
+    B.q[(B.q_head + B.q_n) % REACTOR_BATCH_SLOTS] = k;
+    B.q_n++;
+    pthread_cond_broadcast(&B.cv);
+    pthread_mutex_unlock(&B.mu);
+    return;
+  }
   if (B.parser == PARSER_HOST || B.diag_host)
   {
-    rhp_batch_t b = {
-      .bytes = B.h_bytes, .bytes_rw = B.h_bytes, .offsets = B.h_off, .bytes_size = bytes + RHP_PAD, .n = n,
-      .max_headers = REACTOR_BATCH_HEADERS, .mode = RHP_MODE_HTTP, .reqs = B.h_req, .hdrs = B.h_hdr, .http = B.h_http};
-    (void) rhp_cpu_parse_batch(&b);
+    host_parse(&B, k);
+    if (B.parser == PARSER_GPU)
+      round_done((void *) (intptr_t) B.efd);   /* diagnostic mode keeps the asynchronous protocol */
+    return;
   }
-  else
-  {
-    HIP(hipMemcpyAsync(B.d_bytes, B.h_bytes, bytes + RHP_PAD, hipMemcpyHostToDevice, B.stream));
-    HIP(hipMemcpyAsync(B.d_off, B.h_off, (n + 1) * sizeof *B.h_off, hipMemcpyHostToDevice, B.stream));
-    rhp_batch_t b = {
-      .bytes = B.d_bytes, .bytes_rw = B.d_bytes, .offsets = B.d_off, .bytes_size = bytes + RHP_PAD, .n = n,
-      .max_headers = REACTOR_BATCH_HEADERS, .mode = RHP_MODE_HTTP, .reqs = B.d_req, .hdrs = B.d_hdr, .http = B.d_http,
-      .work = B.d_work};
-    int rc = rhp_parse_batch(&b, B.stream);
-    if (rc != 0)
-      die("rhp_parse_batch", rc);
-    HIP(hipMemcpyAsync(B.h_req, B.d_req, n * sizeof *B.h_req, hipMemcpyDeviceToHost, B.stream));
-    HIP(hipMemcpyAsync(B.h_hdr, B.d_hdr, (size_t) n * REACTOR_BATCH_HEADERS * sizeof *B.h_hdr, hipMemcpyDeviceToHost,
-                       B.stream));
-    HIP(hipMemcpyAsync(B.h_http, B.d_http, n * sizeof *B.h_http, hipMemcpyDeviceToHost, B.stream));
+  HIP(hipMemcpyAsync(s->d_bytes, s->h_bytes, bytes + RHP_PAD, hipMemcpyHostToDevice, B.stream));
+  HIP(hipMemcpyAsync(s->d_off, s->h_off, (n + 1) * sizeof *s->h_off, hipMemcpyHostToDevice, B.stream));
+  rhp_batch_t b = {
+    .bytes = s->d_bytes, .bytes_rw = s->d_bytes, .offsets = s->d_off, .bytes_size = bytes + RHP_PAD, .n = n,
+    .max_headers = REACTOR_BATCH_HEADERS, .mode = RHP_MODE_HTTP, .reqs = s->d_req, .hdrs = s->d_hdr, .http = s->d_http,
+    .work = B.d_work};
+  int rc = rhp_parse_batch(&b, B.stream);
+  if (rc != 0)
+    die("rhp_parse_batch", rc);
+  HIP(hipMemcpyAsync(s->h_req, s->d_req, n * sizeof *s->h_req, hipMemcpyDeviceToHost, B.stream));
+  HIP(hipMemcpyAsync(s->h_hdr, s->d_hdr, (size_t) n * REACTOR_BATCH_HEADERS * sizeof *s->h_hdr, hipMemcpyDeviceToHost,
+                     B.stream));
+  HIP(hipMemcpyAsync(s->h_http, s->d_http, n * sizeof *s->h_http, hipMemcpyDeviceToHost, B.stream));
+  HIP(hipLaunchHostFunc(B.stream, round_done, (void *) (intptr_t) B.efd));
+}
+
+int reactor_batch_completed(void)
+{
+  uint64_t v = 0;
+  if (read(B.efd, &v, sizeof v) != (ssize_t) sizeof v)
+    return 0;
+  return (int) v;
+}
+
+void reactor_batch_wait(void)
+{
+  if (B.parser == PARSER_GPU)
     HIP(hipStreamSynchronize(B.stream));
+  if (B.parser == PARSER_HOST_ASYNC)
+  {
+    pthread_mutex_lock(&B.mu);
+    while (B.q_n)
+      pthread_cond_wait(&B.cv, &B.mu);
+    pthread_mutex_unlock(&B.mu);
+  }
+}
+
+void reactor_batch_result(int k, reactor_batch_result_t *out)
+{
+  slot_t *s = &B.slot[k];
+  if (B.parser == PARSER_GPU && !B.diag_host)
+  {
     /* chunked bodies were de-framed in place in device memory (http.c:155):
-     * bring those bytes back so the caller sees the rewritten input */
-    for (uint32_t i = 0; i < n; i++)
+     * bring those bytes back so the caller sees the rewritten input (the
+     * round's work on the stream is complete: plain copies) */
+    for (uint32_t i = 0; i < s->n; i++)
     {
-      const rhp_http_t *x = &B.h_http[i];
-      if (x->result == 1 && x->body_kind && x->consumed != (uint64_t) B.h_req[i].ret + x->body_len)
-        HIP(hipMemcpy(B.h_bytes + B.h_off[i], (uint8_t *) B.d_bytes + B.h_off[i], x->consumed,
+      const rhp_http_t *x = &s->h_http[i];
+      if (x->result == 1 && x->body_kind && x->consumed != (uint64_t) s->h_req[i].ret + x->body_len)
+        HIP(hipMemcpy(s->h_bytes + s->h_off[i], (uint8_t *) s->d_bytes + s->h_off[i], x->consumed,
                       hipMemcpyDeviceToHost));
     }
   }
   if (B.stats)
   {
     B.st_rounds++;
-    B.st_requests += n;
-    B.st_ns += now_ns() - t0;
+    B.st_requests += s->n;
+    B.st_ns += now_ns() - s->t_submit;
   }
-  out->bytes = B.h_bytes;
-  out->reqs = B.h_req;
-  out->hdrs = B.h_hdr;
-  out->n = n;
-  out->http = B.h_http;
-  return 0;
+  out->bytes = s->h_bytes;
+  out->reqs = s->h_req;
+  out->hdrs = s->h_hdr;
+  out->n = s->n;
+  out->http = s->h_http;
+  out->offsets = s->h_off;
 }

@@ -7,21 +7,34 @@
 #include "rhp.h"
 
 #define REACTOR_BATCH_HEADERS 16u   /* fields_count = 16 per request (server.c:44 of the reference) */
+#define REACTOR_BATCH_SLOTS   2     /* rounds in flight per thread: one parsing, one being packed */
 
 typedef struct reactor_batch_result
 {
   const uint8_t    *bytes;   /* the packed input after the parse (chunked bodies de-framed) */
+  const uint64_t   *offsets; /* n + 1 */
   const rhp_req_t  *reqs;
-  const rhp_hdr_t  *hdrs;    /* REACTOR_BATCH_HEADERS per request, header-major (stride n) */
+  const rhp_hdr_t  *hdrs;    /* REACTOR_BATCH_HEADERS per request, request-major */
   uint32_t          n;
   const rhp_http_t *http;
 } reactor_batch_result_t;
 
-/* staging for `bytes` packed input bytes (+ RHP_PAD) and n segments */
-uint8_t  *reactor_batch_reserve(size_t bytes, uint32_t n);
-uint64_t *reactor_batch_offsets(void);
-/* parse the n segments (offsets[0..n-1], offsets[n] = bytes) in http_read_request mode */
-int       reactor_batch_run(uint32_t n, size_t bytes, reactor_batch_result_t *out);
+/* 1: rounds complete asynchronously (gpu parser) and each completion adds 1 to
+ * the eventfd reactor_batch_fd(); 0: reactor_batch_submit parses in place */
+int       reactor_batch_async(void);
+int       reactor_batch_fd(void);
+/* staging of slot k for `bytes` packed input bytes (+ RHP_PAD) and n segments */
+uint8_t  *reactor_batch_reserve(int k, size_t bytes, uint32_t n);
+uint64_t *reactor_batch_offsets(int k);
+/* parse slot k's n segments (offsets[0..n-1], offsets[n] = bytes) in
+ * http_read_request mode; slots complete in submission order */
+void      reactor_batch_submit(int k, uint32_t n, size_t bytes);
+/* rounds completed since the last call (reads the eventfd; 0 if none) */
+int       reactor_batch_completed(void);
+/* block until every submitted round is complete (teardown) */
+void      reactor_batch_wait(void);
+/* the records of completed slot k */
+void      reactor_batch_result(int k, reactor_batch_result_t *out);
 
 /* records (offsets into base) -> the reference's output iovecs (http.c) */
 struct http_field;

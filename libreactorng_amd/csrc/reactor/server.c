@@ -12,6 +12,14 @@
  * (READY / PROCESSING), the same abort handling, the same -1 -> close and
  * 0 -> wait outcomes.
  *
+ * With the gpu parser a round is asynchronous: it is packed into a batch slot
+ * and submitted, the loop goes on serving sockets, and the round is dispatched
+ * when its completion arrives on the batch eventfd (polled only while rounds
+ * are in flight).  Up to REACTOR_BATCH_SLOTS rounds are in flight per thread:
+ * sessions that received bytes meanwhile are packed into the next slot while
+ * the first parses; a session belongs to one round at a time.  Rounds complete
+ * and dispatch in submission order.
+ *
  * Pipelined input: a session's input is split
  * speculatively after every "\r\n\r\n" and each piece is one request of the
  * batch, so N pipelined requests cost one launch, not N.  A piece's result is
@@ -25,6 +33,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <sys/epoll.h>
 
 #include "reactor.h"
 #include "reactor_batch.h"
@@ -67,6 +76,7 @@ static void server_date_update(void)
 /* ------------------------------------------------------------- session */
 
 static void server_batch_run(reactor_event_t *);
+static void server_rounds_drain(server_t *);
 
 static void server_queue(server_session_t *s)
 {
@@ -170,11 +180,20 @@ typedef struct piece
 
 typedef struct round
 {
+  server_t          *server;
   server_session_t **sessions;
   size_t             n_sessions, cap_sessions;
   piece_t           *pieces;
   size_t             n_pieces, cap_pieces;
 } round_t;
+
+/* the rounds in flight on this thread, in submission order (slot = index) */
+static __thread struct
+{
+  round_t   r[REACTOR_BATCH_SLOTS];
+  int       head, count;
+  reactor_t poll;   /* the batch eventfd, registered while count > 0 */
+} R;
 
 static void *grow(void *p, size_t *cap, size_t need, size_t elem)
 {
@@ -249,7 +268,7 @@ static bool server_session_dispatch(server_session_t *s, const piece_t *pc, size
       break;
     if (x->result != RHP_RET_TOOLONG)
     {
-      const uint64_t off = reactor_batch_offsets()[p->index];
+      const uint64_t off = res->offsets[p->index];
       uint8_t *base = data_base(in);
       if (x->body_kind && x->consumed != (uint64_t) res->reqs[p->index].ret + x->body_len)
         memcpy(base, res->bytes + off, x->consumed);   /* chunked body, de-framed in place */
@@ -274,9 +293,9 @@ static bool server_session_dispatch(server_session_t *s, const piece_t *pc, size
   return !more;
 }
 
-/* RHP_REACTOR_STATS=1: time per round phase (split+pack, parse, dispatch), at exit */
+/* RHP_REACTOR_STATS=1: time per round phase (split+pack+submit, dispatch), at exit */
 static int round_stats = -1;
-static uint64_t rs_pack_ns, rs_parse_ns, rs_dispatch_ns, rs_rounds;
+static uint64_t rs_pack_ns, rs_dispatch_ns, rs_rounds;
 static uint64_t rs_now(void)
 {
   struct timespec ts;
@@ -285,11 +304,11 @@ static uint64_t rs_now(void)
 }
 static void rs_print(void)
 {
-  fprintf(stderr, "server rounds: %llu, split+pack %.1f ms, parse %.1f ms, dispatch %.1f ms\n", (unsigned long long) rs_rounds,
-          (double) rs_pack_ns / 1e6, (double) rs_parse_ns / 1e6, (double) rs_dispatch_ns / 1e6);
+  fprintf(stderr, "server rounds: %llu, split+pack+submit %.1f ms, dispatch %.1f ms\n", (unsigned long long) rs_rounds,
+          (double) rs_pack_ns / 1e6, (double) rs_dispatch_ns / 1e6);
 }
 
-static void server_batch_round(server_t *server, round_t *r)
+static void round_stats_init(void)
 {
   if (round_stats < 0)
   {
@@ -297,12 +316,22 @@ static void server_batch_round(server_t *server, round_t *r)
     if ((round_stats = st && *st == '1'))
       atexit(rs_print);
   }
-  const uint64_t t0 = round_stats ? rs_now() : 0;
+}
+
+/* the queued sessions not already in a round, split into pieces; false: none */
+static bool round_build(server_t *server, round_t *r, size_t *bytes_out)
+{
+  r->server = server;
   r->n_sessions = r->n_pieces = 0;
   size_t bytes = 0;
-  while (!list_is_empty(&server->queue))
+  list_t *it = server->queue.next;
+  while (it != &server->queue)
   {
-    server_session_t *s = container_of(server->queue.next, server_session_t, queued);
+    list_t *nx = it->next;
+    server_session_t *s = container_of(it, server_session_t, queued);
+    it = nx;
+    if (s->in_round)
+      continue;   /* stays queued: parsed in a round after its current one */
     list_unlink(&s->queued);
     if (!(s->flags & SERVER_SESSION_READY) || !stream_is_open(&s->stream))
       continue;
@@ -326,67 +355,125 @@ static void server_batch_round(server_t *server, round_t *r)
     s->exact = false;
     bytes += data_size(in);
   }
-  if (!r->n_sessions)
-    return;
+  *bytes_out = bytes;
+  return r->n_sessions != 0;
+}
 
-  /* pack every session's input, back to back, and parse all pieces at once */
-  if (r->n_pieces)
-  {
-    uint8_t *h = reactor_batch_reserve(bytes, (uint32_t) r->n_pieces);
-    uint64_t *off = reactor_batch_offsets();
-    size_t at = 0, k = 0;
-    for (size_t i = 0; i < r->n_sessions; i++)
-    {
-      data_t in = stream_read(&r->sessions[i]->stream);
-      memcpy(h + at, data_base(in), data_size(in));
-      for (; k < r->n_pieces && r->pieces[k].session == r->sessions[i]; k++)
-        off[k] = at + r->pieces[k].start;
-      at += data_size(in);
-    }
-  }
+/* dispatch a parsed round (slot k) and release its sessions */
+static void round_finish(round_t *r, int k, bool dispatch)
+{
+  const uint64_t t0 = round_stats ? rs_now() : 0;
   reactor_batch_result_t res = {0};
-  const uint64_t t1 = round_stats ? rs_now() : 0;
   if (r->n_pieces)
-    (void) reactor_batch_run((uint32_t) r->n_pieces, bytes, &res);
-  const uint64_t t2 = round_stats ? rs_now() : 0;
-
-  size_t k = 0;
-  for (size_t i = 0; i < r->n_sessions; i++)
+    reactor_batch_result(k, &res);
+  size_t i = 0;
+  for (size_t kk = 0; dispatch && i < r->n_sessions; i++)
   {
     server_session_t *s = r->sessions[i];
-    size_t k0 = k;
-    while (k < r->n_pieces && r->pieces[k].session == s)
-      k++;
-    if (!s->dead && !server_session_dispatch(s, r->pieces + k0, k - k0, &res) && !s->dead)
+    size_t k0 = kk;
+    while (kk < r->n_pieces && r->pieces[kk].session == s)
+      kk++;
+    if (!s->dead && !server_session_dispatch(s, r->pieces + k0, kk - k0, &res) && !s->dead)
     {
       s->exact = true;   /* parse the rest as one piece (exact http_read_request semantics) */
       server_queue(s);
     }
   }
-  for (size_t i = 0; i < r->n_sessions; i++)
+  for (i = 0; i < r->n_sessions; i++)
   {
     r->sessions[i]->in_round = false;
     if (r->sessions[i]->dead)
       free(r->sessions[i]);
   }
+  server_t *server = r->server;
+  r->n_sessions = r->n_pieces = 0;
+  if (dispatch && !list_is_empty(&server->queue) && !server->batch)
+    server->batch = reactor_next(server_batch_run, server);   /* sessions that waited for this round */
   if (round_stats)
+    rs_dispatch_ns += rs_now() - t0;
+}
+
+static void server_batch_ready(reactor_event_t *event)
+{
+  (void) event;
+  for (int c = reactor_batch_completed(); c > 0 && R.count; c--)
   {
-    const uint64_t t3 = rs_now();
-    rs_pack_ns += t1 - t0;
-    rs_parse_ns += t2 - t1;
-    rs_dispatch_ns += t3 - t2;
-    rs_rounds++;
+    const int k = R.head;
+    R.head = (R.head + 1) % REACTOR_BATCH_SLOTS;
+    R.count--;
+    round_finish(&R.r[k], k, true);
+  }
+  if (!R.count && R.poll)
+  {
+    reactor_poll_remove(R.poll);
+    R.poll = 0;
   }
 }
 
 static void server_batch_run(reactor_event_t *event)
 {
   server_t *server = event->state;
-  round_t r = {0};
   server->batch = 0;
-  server_batch_round(server, &r);
-  free(r.sessions);
-  free(r.pieces);
+  round_stats_init();
+  if (R.count == REACTOR_BATCH_SLOTS)
+    return;   /* every slot in flight: the next completion schedules this again */
+  const uint64_t t0 = round_stats ? rs_now() : 0;
+  const int k = (R.head + R.count) % REACTOR_BATCH_SLOTS;
+  round_t *r = &R.r[k];
+  size_t bytes = 0;
+  if (!round_build(server, r, &bytes))
+    return;
+  /* pack every session's input, back to back, and parse all pieces at once */
+  if (r->n_pieces)
+  {
+    uint8_t *h = reactor_batch_reserve(k, bytes, (uint32_t) r->n_pieces);
+    uint64_t *off = reactor_batch_offsets(k);
+    size_t at = 0, q = 0;
+    for (size_t i = 0; i < r->n_sessions; i++)
+    {
+      data_t in = stream_read(&r->sessions[i]->stream);
+      memcpy(h + at, data_base(in), data_size(in));
+      for (; q < r->n_pieces && r->pieces[q].session == r->sessions[i]; q++)
+        off[q] = at + r->pieces[q].start;
+      at += data_size(in);
+    }
+    reactor_batch_submit(k, (uint32_t) r->n_pieces, bytes);
+  }
+  if (round_stats)
+  {
+    rs_pack_ns += rs_now() - t0;
+    rs_rounds++;
+  }
+  if (!r->n_pieces || !reactor_batch_async())
+  {
+    round_finish(r, k, true);   /* parsed in place (host parser), or nothing to parse */
+    return;
+  }
+  R.count++;
+  if (!R.poll)
+    R.poll = reactor_poll(server_batch_ready, NULL, reactor_batch_fd(), EPOLLIN);
+}
+
+/* teardown: every round in flight completes; this server's are released
+ * without dispatch, other servers' are dispatched */
+static void server_rounds_drain(server_t *server)
+{
+  if (!R.count)
+    return;
+  reactor_batch_wait();
+  (void) reactor_batch_completed();
+  while (R.count)
+  {
+    const int k = R.head;
+    R.head = (R.head + 1) % REACTOR_BATCH_SLOTS;
+    R.count--;
+    round_finish(&R.r[k], k, R.r[k].server != server);
+  }
+  if (R.poll)
+  {
+    reactor_poll_remove(R.poll);
+    R.poll = 0;
+  }
 }
 
 /* -------------------------------------------------------------- public */
@@ -403,6 +490,7 @@ void server_destruct(server_t *server)
 {
   server_close(server);
   timeout_destruct(&server->timeout);
+  server_rounds_drain(server);
   while (!list_is_empty(&server->sessions))
   {
     server_session_t *s = container_of(server->sessions.next, server_session_t, link);

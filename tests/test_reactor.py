@@ -67,6 +67,46 @@ def test_server_cases_host_parser():
     assert "config1 16 pipelined   responses 16  callbacks 16" in out
 
 
+def test_server_cases_host_async_parser():
+    """Asynchronous rounds (batch.c "host-async": the gpu mode's slots and
+    eventfd completion, parsed on a worker thread): the same cases."""
+    out = _run([os.path.join(BIN, "server_test"), "32", "64"], "host-async")
+    assert "parser: host-async" in out and "OK (0 failures)" in out
+    assert "config1 16 pipelined   responses 16  callbacks 16" in out
+
+
+def _burst(parser, conns=64, pipelined=64, reps=5):
+    """burst_test: conns x pipelined requests land before the loop starts, so
+    rounds hold conns x pipelined requests; req/s per burst (the first burst,
+    which pays first-use costs, is dropped)."""
+    env = dict(os.environ, RHP_REACTOR_PARSER=parser, RHP_REACTOR_STATS="1")
+    p = subprocess.run([os.path.join(BIN, "burst_test"), str(conns), str(pipelined), str(reps)], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and "OK (0 failures)" in p.stdout, p.stdout + p.stderr
+    rates = [float(x) for x in re.findall(r"\(([0-9.]+) req/s\)", p.stdout)]
+    per_round = float(re.search(r"\(([0-9.]+) per round\)", p.stderr).group(1))
+    return sorted(rates[1:])[len(rates[1:]) // 2], per_round, p.stdout + p.stderr
+
+
+@pytest.mark.parametrize("parser", ["host", "host-async"])
+def test_burst_rounds_host_parsers(parser):
+    rate, per_round, out = _burst(parser, reps=3)
+    assert per_round >= 4000, out
+
+
+@pytest.mark.gpu
+def test_burst_rounds_gpu_vs_host():
+    """4096-request rounds (64 connections x 64 pipelined): the server with the
+    MI355X parser (asynchronous rounds) against the host parser, same process
+    layout; both numbers are printed and recorded in DESIGN.md."""
+    gpu, gpu_round, out_g = _burst("gpu")
+    host, host_round, out_h = _burst("host")
+    print(f"burst req/s: gpu {gpu:.0f} ({gpu_round:.0f} requests/round), host {host:.0f} ({host_round:.0f})")
+    print(out_g, out_h)
+    assert gpu_round >= 4000 and host_round >= 4000
+    assert gpu >= 0.8 * host, (gpu, host)
+
+
 @pytest.mark.gpu
 def test_server_cases_gpu_batch_parser():
     """The same cases with sessions parsed by rhp_parse_batch on the MI355X."""
@@ -84,7 +124,9 @@ def test_reactor_host_code_asan_ubsan_clean(tmp_path):
     subprocess.check_call(["make", "-s", "-C", os.path.join(LIB, "csrc"), "asan"])
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
     asan = os.path.join(LIB, "asan")
-    for args in ([os.path.join(asan, "http_test"), _vectors(tmp_path)], [os.path.join(asan, "server_test"), "8", "16"]):
-        p = subprocess.run(args, env=dict(env, RHP_REACTOR_PARSER="host"), capture_output=True, text=True, timeout=300)
+    for args, parser in (([os.path.join(asan, "http_test"), _vectors(tmp_path)], "host"),
+                         ([os.path.join(asan, "server_test"), "8", "16"], "host"),
+                         ([os.path.join(asan, "server_test"), "8", "16"], "host-async")):
+        p = subprocess.run(args, env=dict(env, RHP_REACTOR_PARSER=parser), capture_output=True, text=True, timeout=300)
         assert p.returncode == 0 and "OK (0 failures)" in p.stdout, p.stdout + p.stderr
         assert "runtime error" not in p.stderr and "AddressSanitizer" not in p.stderr, p.stderr

@@ -1,10 +1,13 @@
 """Diagnostic: per-section shader cycles of rhp_dfa_kernel (RHP_STAMPS build,
-RHP_LIB=librhp_x_stamps.so) for configs 2, 3, 5 at bench's layouts."""
+RHP_LIB=librhp_x_stamps.so) for configs 2, 3, 5 at bench's layouts, and the
+launch's timeline from the realtime marks (entry, loop start, loop end, exit;
+100 MHz ticks)."""
 import ctypes, os, sys
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import libreactorng_amd as rhp
+SLOTS = 12
 lib = rhp.lib()
 lib.rhp_debug_stamps.argtypes = [ctypes.c_void_p]
 names = ["A wait window", "C-E switch/refill/issue", "decode", "walk", "finalize/handover"]
@@ -22,9 +25,9 @@ for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, 1), (r
     dbs[0].launch()
     b.record()
     torch.cuda.synchronize()
-    st = np.zeros(8192 * 8, dtype=np.uint64)
+    st = np.zeros(8192 * SLOTS, dtype=np.uint64)
     assert lib.rhp_debug_stamps(st.ctypes.data) == 0
-    st = st.reshape(8192, 8).astype(np.float64)
+    st = st.reshape(8192, SLOTS).astype(np.float64)
     used = st[:, 5] > 0
     tot = st[used, :5].sum(axis=0)
     it = st[used, 5].sum()
@@ -32,4 +35,27 @@ for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, 1), (r
           f"({it / used.sum():.1f} per wave), cycles per iteration per wave:")
     for k in range(5):
         print(f"   {names[k]:26s} {tot[k] / it:8.0f}  ({100 * tot[k] / tot.sum():.1f} %)")
-    print(f"   per wave: {st[used, :5].sum(axis=1).mean():.0f} cycles in the loop", flush=True)
+    loop = st[used, :5].sum(axis=1)
+    print(f"   per wave: {loop.mean():.0f} cycles in the loop (min {loop.min():.0f}, max {loop.max():.0f})")
+    rt = st[used, 6:10] * 10.0 / 1000.0   # us
+    t0 = rt[:, 0].min()
+    rt = rt - t0
+    q = lambda v: f"{np.percentile(v, 0):6.1f} {np.percentile(v, 50):6.1f} {np.percentile(v, 99):6.1f} {v.max():6.1f}"
+    print("   timeline us from the first entry (min / median / p99 / max):")
+    print(f"     entry       {q(rt[:, 0])}")
+    print(f"     loop start  {q(rt[:, 1])}   prologue {q(rt[:, 1] - rt[:, 0])}")
+    print(f"     loop end    {q(rt[:, 2])}   loop     {q(rt[:, 2] - rt[:, 1])}")
+    print(f"     exit        {q(rt[:, 3])}   replay   {q(rt[:, 3] - rt[:, 2])}")
+    # by wave slot in the workgroup (dispatch age): iterations and loop end
+    idx = np.nonzero(used)[0] % 16
+    its = st[used, 5]
+    print("   by wave slot: iterations / loop end us (mean)")
+    print("     " + " ".join(f"{its[idx == k].mean():5.1f}" for k in range(16)))
+    print("     " + " ".join(f"{rt[idx == k, 2].mean():5.1f}" for k in range(16)))
+    wg = np.nonzero(used)[0] // 16
+    ends = np.array([rt[wg == g, 2].max() for g in np.unique(wg)])
+    firsts = np.array([rt[wg == g, 2].min() for g in np.unique(wg)])
+    nw_, ni_ = st[used, 10], st[used, 11]
+    print("   by wave slot: lane occupancy (walked / (walked + idle))")
+    print("     " + " ".join(f"{nw_[idx == k].sum() / (nw_[idx == k].sum() + ni_[idx == k].sum()):5.2f}" for k in range(16)))
+    print(f"   workgroups: last wave's loop end {q(ends)}; first wave's {q(firsts)}", flush=True)

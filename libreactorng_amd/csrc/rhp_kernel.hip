@@ -103,9 +103,13 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 #ifdef RHP_STAMPS
-/* diagnostic build only: per-wave shader-cycle sums per loop section, stored by
- * each wave's lane 0 into a buffer of its own (never read by the kernel) */
-__device__ unsigned long long g_stamps[8192 * 8];
+/* diagnostic build only: per-wave shader-cycle sums per loop section and
+ * realtime (100 MHz) marks, stored by each wave's lane 0 into a buffer of its
+ * own (never read by the kernel): slots 0-4 section cycles, 5 iterations,
+ * 6 entry, 7 loop start, 8 loop end, 9 exit, 10 lane-windows walked,
+ * 11 lane-iterations without a window to walk */
+enum : uint32_t { kStampSlots = 12 };
+__device__ unsigned long long g_stamps[8192 * kStampSlots];
 #define RHP_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); (t) = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
@@ -325,19 +329,12 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
+#ifdef RHP_STAMPS
+  const unsigned long long rt_entry = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef RHP_CLOCK
   const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
-
-  {
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(&g_table);
-    u32x4 *dst = reinterpret_cast<u32x4 *>(lds);
-    for (uint32_t k = tid; k < kTable2Bytes / 16; k += WAVES * 64) dst[k] = src[k];
-    /* pool counters and the long-request bitmap start at zero */
-    for (uint32_t k = tid; k < kPoolWords + kOrderSpan / 32; k += WAVES * 64)
-      reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave)[k] = 0;
-  }
-  __syncthreads();
 
   const uint32_t maxh = p.max_headers;
   const bool http = p.mode == RHP_MODE_HTTP;
@@ -351,6 +348,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * Window addresses are u32 byte offsets from `base` (the 4-aligned start of
    * the range; the host keeps a batch below 4 GiB). */
   const uint32_t wg_lo = min(blockIdx.x * p.span, p.n), wg_hi = min(wg_lo + p.span, p.n);
+  /* the first WAVES * 64 requests of the range go to the threads in order
+   * (first_n); refills hand out the rest from the LDS counter */
+  const uint32_t first_n = min(wg_hi - wg_lo, (uint32_t) (WAVES * 64));
   uint32_t *wg_counter = reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave);
   uint32_t *wg_deferred = wg_counter + 1;   /* some request of the range needs the replay */
   /* Long requests first.  With lengths as uneven as config 3's, the requests
@@ -365,7 +365,19 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   bool list_dry = !order_on;
   bool first_iter = true;   /* the list is complete only after the scan (before the loop) */
   bool pool_dry = wg_lo >= wg_hi;
-  const uint64_t base = pool_dry ? 0 : (p.offsets[wg_lo] & ~(uint64_t) 3);
+  /* The prologue's global reads all go out at once (one round trip): the
+   * table, the range's end offsets and every thread's first request. */
+  u32x4 tab[(kTable2Bytes / 16 + WAVES * 64 - 1) / (WAVES * 64)];
+  {
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(&g_table);
+#pragma unroll
+    for (uint32_t j = 0; j < sizeof tab / sizeof tab[0]; j++) {
+      const uint32_t k = tid + j * WAVES * 64;
+      if (k < kTable2Bytes / 16) tab[j] = src[k];
+    }
+  }
+  const uint64_t o_lo = pool_dry ? 0 : p.offsets[wg_lo], o_hi = pool_dry ? 0 : p.offsets[wg_hi];
+  const uint64_t base = o_lo & ~(uint64_t) 3;
   const uint8_t *wbytes = p.bytes + base;
 
   /* ---- walk state (the request whose window landed) ---- */
@@ -443,10 +455,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   /* the long-request scan (see order_on), once, over the part of the range the
    * first refill did not hand out */
   auto scan_long = [&]() {
-    const uint32_t span_n = wg_hi - wg_lo, first_n = min(span_n, (uint32_t) (WAVES * 64));
+    const uint32_t span_n = wg_hi - wg_lo;
     if (span_n <= first_n) return;
     /* long: length * count > 2 * the range's bytes (no division) */
-    const uint64_t twice = 2u * (p.offsets[wg_hi] - p.offsets[wg_lo]);
+    const uint64_t twice = 2u * (o_hi - o_lo);
     /* a wave scans its slice only if its own first requests (offsets already
      * loaded) include a long one: uniform batches skip the scan */
     if (!__ballot(pend_ok && (uint64_t) (pend_o1 - pend_o0) * span_n > twice)) return;
@@ -721,12 +733,23 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #undef RHP_ISSUE_LOADS
   };
 
-  refill_pend();
+  if (tid < first_n) take(wg_lo + tid);
+  /* the table into LDS, the pool counter past the requests handed out, the
+   * long-request bitmap cleared */
+#pragma unroll
+  for (uint32_t j = 0; j < sizeof tab / sizeof tab[0]; j++) {
+    const uint32_t k = tid + j * WAVES * 64;
+    if (k < kTable2Bytes / 16) reinterpret_cast<u32x4 *>(lds)[k] = tab[j];
+  }
+  for (uint32_t k = tid; k < kPoolWords + kOrderSpan / 32; k += WAVES * 64)
+    reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave)[k] = k == 0 ? first_n : 0u;
   /* The first windows: issue them, then (while they land) the long-request
-   * scan; the barrier makes the list complete before any wave's next refill. */
+   * scan; the barriers make the pool area initialized before the scan and the
+   * list complete before any wave's next refill. */
   wait_vm0();   /* the pending offsets */
   nw = pend_ok ? ((pend_o0 & ~3u) - (uint32_t) base) | 2u : 0u;
   issue();
+  __syncthreads();
   if (order_on) scan_long();
   __syncthreads();
   first_iter = false;
@@ -741,6 +764,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    */
 #ifdef RHP_STAMPS
   unsigned long long t0 = 0, t1 = 0, acc[6] = {0, 0, 0, 0, 0, 0};
+  const unsigned long long rt_loop = __builtin_amdgcn_s_memrealtime();
+  unsigned long long n_walk = 0, n_idle = 0;
 #endif
   for (;;) {
     RHP_STAMP(t0);
@@ -796,6 +821,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     RHP_STAMP(t1); acc[2] += t1 - t0; t0 = t1;
 #endif
     const bool any_walk = __builtin_amdgcn_ballot_w64(walking) != 0;
+#ifdef RHP_STAMPS
+    n_walk += __popcll(__builtin_amdgcn_ballot_w64(walking));
+    n_idle += __popcll(__builtin_amdgcn_ballot_w64(!walking));
+#endif
     const bool any_dec = __builtin_amdgcn_ballot_w64(dhas) != 0;
     if (any_walk) {
       if (!walking) st = kPark;   /* idle lanes step in the parked terminal state */
@@ -852,7 +881,12 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #ifdef RHP_STAMPS
   if (lane == 0) {
     const uint32_t w = (blockIdx.x * WAVES + (tid >> 6)) % 8192;
-    for (int k = 0; k < 6; k++) g_stamps[w * 8 + k] = acc[k];
+    for (int k = 0; k < 6; k++) g_stamps[w * kStampSlots + k] = acc[k];
+    g_stamps[w * kStampSlots + 6] = rt_entry;
+    g_stamps[w * kStampSlots + 7] = rt_loop;
+    g_stamps[w * kStampSlots + 8] = __builtin_amdgcn_s_memrealtime();
+    g_stamps[w * kStampSlots + 10] = n_walk;
+    g_stamps[w * kStampSlots + 11] = n_idle;
   }
 #endif
 #ifdef RHP_CLOCK
@@ -889,6 +923,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       }
     }
   }
+#ifdef RHP_STAMPS
+  if (lane == 0) g_stamps[((blockIdx.x * WAVES + (tid >> 6)) % 8192) * kStampSlots + 9] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 /* Exact-path-only kernel: one request per thread, grid-stride (RHP_IMPL_EXACT). */
@@ -961,7 +998,7 @@ extern "C" {
 const char *rhp_version(void) { return "rhp 0.5.0 (gfx950)"; }
 
 #ifdef RHP_STAMPS
-/* diagnostic build only: the per-wave section cycle sums (8192 x 8 u64) */
+/* diagnostic build only: the per-wave stamps (8192 x kStampSlots u64) */
 int rhp_debug_stamps(unsigned long long *host)
 {
   return (int) hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(g_stamps), 0, hipMemcpyDeviceToHost);

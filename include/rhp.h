@@ -180,8 +180,8 @@ typedef struct rhp_resp_batch {
 
 #define RHP_RESP_WORK_WORDS(n) (((uint64_t) (n) + 4095u) / 4096u + 1u)
 
-/* Launch status as rhp_parse_batch; five kernels on `stream` (sizes, three scan
- * passes, copy). */
+/* Launch status as rhp_parse_batch; four kernels on `stream` (sizes with tile
+ * sums, two scan passes, copy). */
 int rhp_write_responses(const rhp_resp_batch_t *batch, void *stream);
 
 

@@ -18,6 +18,12 @@
  * "host-async": the same parser on a worker thread with the gpu mode's
  * completion protocol (slots, eventfd), so the CPU suite exercises the
  * server's pipelined rounds.
+ *
+ * Replies (RHP_REACTOR_WRITER): "gpu" serializes the replies a round's
+ * dispatch produced in one rhp_write_responses call (http_write_response for
+ * the whole round, include/rhp.h); "host-batch" runs the same round-batched
+ * protocol with the host serializer (CPU tests); unset or "host": each reply
+ * is written as the reference does, when the handler responds.
  */
 #define __HIP_PLATFORM_AMD__ 1
 #include <errno.h>
@@ -67,6 +73,12 @@ typedef struct batch_state
   pthread_mutex_t mu;
   pthread_cond_t  cv;
   int             q[REACTOR_BATCH_SLOTS], q_head, q_n;
+  /* the round-batched writer */
+  int             writer;
+  size_t          w_cap_arena, w_cap_n, w_cap_f, w_cap_out;
+  void           *dw_arena, *dw_resps, *dw_fields, *dw_out, *dw_off, *dw_work;
+  uint8_t        *hw_out;
+  uint64_t       *hw_off;
 } batch_state_t;
 
 static __thread batch_state_t B;   /* one parser per reactor thread */
@@ -370,4 +382,126 @@ void reactor_batch_result(int k, reactor_batch_result_t *out)
   out->n = s->n;
   out->http = s->h_http;
   out->offsets = s->h_off;
+}
+
+enum { WRITER_HOST, WRITER_HOST_BATCH, WRITER_GPU };
+
+int reactor_batch_writer(void)
+{
+  (void) parser();
+  if (B.writer == 0)
+  {
+    const char *e = getenv("RHP_REACTOR_WRITER");
+    B.writer = 1 + (!e ? WRITER_HOST : strcmp(e, "gpu") == 0 ? WRITER_GPU : strcmp(e, "host-batch") == 0 ? WRITER_HOST_BATCH
+                                                                                                        : WRITER_HOST);
+    if (B.writer == 1 + WRITER_GPU && B.parser != PARSER_GPU)
+    {
+      /* the gpu writer shares the gpu parser's stream */
+      fprintf(stderr, "reactor: RHP_REACTOR_WRITER=gpu needs RHP_REACTOR_PARSER=gpu\n");
+      abort();
+    }
+  }
+  return B.writer - 1 != WRITER_HOST;
+}
+
+static void grow_dev(void **p, size_t *cap, size_t need)
+{
+  if (need <= *cap)
+    return;
+  size_t c = *cap ? *cap : 1u << 16;
+  while (c < need)
+    c *= 2;
+  dev_free(p);
+  HIP(hipMalloc(p, c));
+  *cap = c;
+}
+
+/* n replies in one pass: out_off[0..n] and the bytes out[0, out_off[n]) */
+void reactor_batch_write(const uint8_t *arena, size_t arena_n, const rhp_resp_t *resps, uint32_t n,
+                         const rhp_resp_field_t *fields, uint32_t n_fields, const char *date, const uint8_t **out,
+                         const uint64_t **out_off)
+{
+  if (B.writer - 1 == WRITER_HOST_BATCH)
+  {
+    /* the host serializer, into one buffer in reply order */
+    static __thread buffer_t buf;
+    static __thread uint64_t *off;
+    static __thread size_t cap;
+    if (n + 1 > cap)
+    {
+      cap = n + 1 > 2 * cap ? n + 1 : 2 * cap;
+      if (!(off = realloc(off, cap * sizeof *off)))
+        abort();
+    }
+    buffer_clear(&buf);
+    stream_t tmp;   /* http_write_response appends to a stream's output buffer */
+    memset(&tmp, 0, sizeof tmp);
+    tmp.output = buf;
+    for (uint32_t i = 0; i < n; i++)
+    {
+      off[i] = buffer_size(&tmp.output);
+      const rhp_resp_t *r = &resps[i];
+      http_field_t f[64];
+      const uint32_t nf = r->fields_count < 64 ? r->fields_count : 64;
+      for (uint32_t k = 0; k < nf; k++)
+        f[k] = http_field_define(data(arena + fields[r->fields_first + k].name.off, fields[r->fields_first + k].name.len),
+                                 data(arena + fields[r->fields_first + k].value.off, fields[r->fields_first + k].value.len));
+      http_write_response(&tmp, data(arena + r->status.off, r->status.len), data(date, RHP_DATE_LEN),
+                          data(arena + r->type.off, r->type.len), data(arena + r->body.off, r->body.len), f, nf);
+    }
+    off[n] = buffer_size(&tmp.output);
+    buf = tmp.output;
+    *out = buffer_base(&buf);
+    *out_off = off;
+    (void) arena_n;
+    (void) n_fields;
+    return;
+  }
+  /* gpu: H2D of the round's replies, rhp_write_responses, D2H (synchronous) */
+  grow_dev(&B.dw_arena, &B.w_cap_arena, arena_n + 16);
+  size_t cap_n = B.w_cap_n;
+  grow_dev(&B.dw_resps, &B.w_cap_n, (size_t) n * sizeof *resps + 16);
+  if (B.w_cap_n != cap_n || !B.hw_off)
+  {
+    dev_free(&B.dw_off);
+    dev_free(&B.dw_work);
+    if (B.hw_off)
+      (void) hipHostFree(B.hw_off);
+    const size_t rn = B.w_cap_n / sizeof *resps + 1;
+    HIP(hipMalloc(&B.dw_off, rn * sizeof(uint64_t)));
+    HIP(hipMalloc(&B.dw_work, RHP_RESP_WORK_WORDS(rn) * sizeof(uint64_t)));
+    HIP(hipHostMalloc((void **) &B.hw_off, rn * sizeof(uint64_t), hipHostMallocDefault));
+  }
+  grow_dev(&B.dw_fields, &B.w_cap_f, (size_t) n_fields * sizeof *fields + 16);
+  HIP(hipMemcpyAsync(B.dw_arena, arena, arena_n, hipMemcpyHostToDevice, B.stream));
+  HIP(hipMemcpyAsync(B.dw_resps, resps, (size_t) n * sizeof *resps, hipMemcpyHostToDevice, B.stream));
+  if (n_fields)
+    HIP(hipMemcpyAsync(B.dw_fields, fields, (size_t) n_fields * sizeof *fields, hipMemcpyHostToDevice, B.stream));
+  for (int pass = 0; pass < 2; pass++)
+  {
+    rhp_resp_batch_t w = {.arena = B.dw_arena, .resps = B.dw_resps, .fields = n_fields ? B.dw_fields : NULL, .n = n,
+                          .date_len = RHP_DATE_LEN, .date = date, .out_off = B.dw_off, .out = B.dw_out,
+                          .out_size = B.w_cap_out, .work = B.dw_work};
+    int rc = rhp_write_responses(&w, B.stream);
+    if (rc != 0)
+      die("rhp_write_responses", rc);
+    HIP(hipMemcpyAsync(B.hw_off, B.dw_off, ((size_t) n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, B.stream));
+    HIP(hipStreamSynchronize(B.stream));
+    if (B.hw_off[n] <= B.w_cap_out)
+      break;
+    /* the output did not fit: grow it and write again (rhp.h) */
+    size_t c = B.w_cap_out ? B.w_cap_out : 1u << 20;
+    while (c < B.hw_off[n])
+      c *= 2;
+    dev_free(&B.dw_out);
+    HIP(hipMalloc(&B.dw_out, c));
+    if (B.hw_out)
+      (void) hipHostFree(B.hw_out);
+    HIP(hipHostMalloc((void **) &B.hw_out, c, hipHostMallocDefault));
+    B.w_cap_out = c;
+  }
+  HIP(hipMemcpyAsync(B.hw_out, B.dw_out, B.hw_off[n], hipMemcpyDeviceToHost, B.stream));
+  HIP(hipStreamSynchronize(B.stream));
+  *out = B.hw_out;
+  *out_off = B.hw_off;
 }

@@ -36,6 +36,15 @@ void      reactor_batch_wait(void);
 /* the records of completed slot k */
 void      reactor_batch_result(int k, reactor_batch_result_t *out);
 
+/* 1: replies produced while a round is dispatched are serialized together
+ * after it (RHP_REACTOR_WRITER=gpu | host-batch); 0: written at once */
+int       reactor_batch_writer(void);
+/* serialize n replies (spans of `arena`) as http_write_response does; out and
+ * out_off (n + 1 offsets) stay valid until the next call */
+void      reactor_batch_write(const uint8_t *arena, size_t arena_n, const rhp_resp_t *resps, uint32_t n,
+                              const rhp_resp_field_t *fields, uint32_t n_fields, const char *date, const uint8_t **out,
+                              const uint64_t **out_off);
+
 /* records (offsets into base) -> the reference's output iovecs (http.c) */
 struct http_field;
 void reactor_http_fill(const uint8_t *base, const rhp_req_t *r, const rhp_hdr_t *h, size_t hs, const rhp_http_t *x,

@@ -195,6 +195,7 @@ static __thread struct
   reactor_t poll;   /* the batch eventfd, registered while count > 0 */
 } R;
 
+
 static void *grow(void *p, size_t *cap, size_t need, size_t elem)
 {
   if (need <= *cap)
@@ -207,6 +208,76 @@ static void *grow(void *p, size_t *cap, size_t need, size_t elem)
     abort();
   *cap = c;
   return p;
+}
+
+/* Round-batched replies (reactor_batch_writer): while a round is dispatched,
+ * server_respond records each reply (its strings copied into an arena), and
+ * the round's sessions are flushed only after one reactor_batch_write call has
+ * serialized all of them, in reply order. */
+static __thread struct
+{
+  bool               on;          /* collecting: a round is being dispatched */
+  uint8_t           *arena;
+  size_t             arena_n, arena_cap;
+  rhp_resp_t        *resps;
+  server_session_t **owner;
+  size_t             n, cap, cap_owner;
+  rhp_resp_field_t  *fields;
+  size_t             nf, cap_f;
+} W;
+
+static rhp_span_t w_span(data_t d)
+{
+  const size_t n = data_size(d);
+  W.arena = grow(W.arena, &W.arena_cap, W.arena_n + n + 4, 1);
+  if (n)
+    memcpy(W.arena + W.arena_n, data_base(d), n);
+  const rhp_span_t sp = {.off = (uint32_t) W.arena_n, .len = (uint32_t) n};
+  W.arena_n += n;
+  return sp;
+}
+
+static void w_record(server_session_t *s, string_t status, string_t type, data_t body, http_field_t *fields,
+                     size_t fields_count)
+{
+  W.resps = grow(W.resps, &W.cap, W.n + 1, sizeof *W.resps);
+  W.owner = grow(W.owner, &W.cap_owner, W.n + 1, sizeof *W.owner);
+  W.fields = grow(W.fields, &W.cap_f, W.nf + fields_count + 1, sizeof *W.fields);
+  rhp_resp_t *r = &W.resps[W.n];
+  r->status = w_span(status);
+  r->type = w_span(type);
+  r->body = w_span(body);
+  r->fields_first = (uint32_t) W.nf;
+  r->fields_count = (uint32_t) fields_count;
+  for (size_t k = 0; k < fields_count; k++)
+  {
+    W.fields[W.nf].name = w_span(fields[k].name);
+    W.fields[W.nf].value = w_span(fields[k].value);
+    W.nf++;
+  }
+  W.owner[W.n++] = s;
+}
+
+/* serialize the recorded replies into their sessions' output, then flush the
+ * round's sessions */
+static void w_flush_round(round_t *r)
+{
+  if (W.n)
+  {
+    const uint8_t *out;
+    const uint64_t *off;
+    reactor_batch_write(W.arena, W.arena_n, W.resps, (uint32_t) W.n, W.fields, (uint32_t) W.nf, server_date, &out, &off);
+    for (size_t i = 0; i < W.n; i++)
+    {
+      server_session_t *s = W.owner[i];
+      if (!s->dead && stream_is_open(&s->stream))
+        stream_write(&s->stream, data(out + off[i], off[i + 1] - off[i]));
+    }
+  }
+  W.n = W.nf = W.arena_n = 0;
+  for (size_t i = 0; i < r->n_sessions; i++)
+    if (!r->sessions[i]->dead && stream_is_open(&r->sessions[i]->stream))
+      stream_flush(&r->sessions[i]->stream);
 }
 
 static const uint8_t *find_crlfcrlf(const uint8_t *p, const uint8_t *end)
@@ -289,7 +360,8 @@ static bool server_session_dispatch(server_session_t *s, const piece_t *pc, size
     s->abort = NULL;
     s->flags &= ~SERVER_SESSION_PROCESSING;
   }
-  stream_flush(&s->stream);
+  if (!W.on)
+    stream_flush(&s->stream);   /* round-batched replies: flushed after the round's write (w_flush_round) */
   return !more;
 }
 
@@ -367,6 +439,7 @@ static void round_finish(round_t *r, int k, bool dispatch)
   if (r->n_pieces)
     reactor_batch_result(k, &res);
   size_t i = 0;
+  W.on = dispatch && reactor_batch_writer();
   for (size_t kk = 0; dispatch && i < r->n_sessions; i++)
   {
     server_session_t *s = r->sessions[i];
@@ -378,6 +451,11 @@ static void round_finish(round_t *r, int k, bool dispatch)
       s->exact = true;   /* parse the rest as one piece (exact http_read_request semantics) */
       server_queue(s);
     }
+  }
+  if (W.on)
+  {
+    W.on = false;
+    w_flush_round(r);
   }
   for (i = 0; i < r->n_sessions; i++)
   {
@@ -541,7 +619,10 @@ void server_respond(server_session_t *session, string_t status, string_t type, d
   session->flags |= SERVER_SESSION_READY;
   if (reactor_likely(stream_is_open(&session->stream)))
   {
-    http_write_response(&session->stream, status, data(server_date, 29), type, body, fields, fields_count);
+    if (W.on && (session->flags & SERVER_SESSION_PROCESSING) && session->in_round)
+      w_record(session, status, type, body, fields, fields_count);   /* serialized with the round's replies */
+    else
+      http_write_response(&session->stream, status, data(server_date, 29), type, body, fields, fields_count);
     if (!(session->flags & SERVER_SESSION_PROCESSING))
     {
       stream_flush(&session->stream);

@@ -107,8 +107,9 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
  * realtime (100 MHz) marks, stored by each wave's lane 0 into a buffer of its
  * own (never read by the kernel): slots 0-4 section cycles, 5 iterations,
  * 6 entry, 7 loop start, 8 loop end, 9 exit, 10 lane-windows walked,
- * 11 lane-iterations without a window to walk */
-enum : uint32_t { kStampSlots = 12 };
+ * 11 lane-iterations without a window to walk, 12 of them while the pool
+ * still had requests, 13 iterations after the pool ran dry */
+enum : uint32_t { kStampSlots = 16 };
 __device__ unsigned long long g_stamps[8192 * kStampSlots];
 #define RHP_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); (t) = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0); } while (0)
@@ -765,7 +766,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #ifdef RHP_STAMPS
   unsigned long long t0 = 0, t1 = 0, acc[6] = {0, 0, 0, 0, 0, 0};
   const unsigned long long rt_loop = __builtin_amdgcn_s_memrealtime();
-  unsigned long long n_walk = 0, n_idle = 0;
+  unsigned long long n_walk = 0, n_idle = 0, n_idle_live = 0, n_dry = 0;
 #endif
   for (;;) {
     RHP_STAMP(t0);
@@ -824,6 +825,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #ifdef RHP_STAMPS
     n_walk += __popcll(__builtin_amdgcn_ballot_w64(walking));
     n_idle += __popcll(__builtin_amdgcn_ballot_w64(!walking));
+    if (!pool_dry) n_idle_live += __popcll(__builtin_amdgcn_ballot_w64(!walking));
+    else n_dry++;
 #endif
     const bool any_dec = __builtin_amdgcn_ballot_w64(dhas) != 0;
     if (any_walk) {
@@ -887,6 +890,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     g_stamps[w * kStampSlots + 8] = __builtin_amdgcn_s_memrealtime();
     g_stamps[w * kStampSlots + 10] = n_walk;
     g_stamps[w * kStampSlots + 11] = n_idle;
+    g_stamps[w * kStampSlots + 12] = n_idle_live;
+    g_stamps[w * kStampSlots + 13] = n_dry;
   }
 #endif
 #ifdef RHP_CLOCK

@@ -4,19 +4,26 @@
  * http_write_response (src/reactor/http.c:286-297, with _basic :236-259 and
  * _extended :261-284) for n responses at once, so the reactor's response side can
  * run as one device pass per round like the parse side.
- * Three launches on the caller's stream:
+ * Four launches on the caller's stream:
  *
- *   rhp_resp_size_kernel   thread per response: its size, exactly the sum the
- *                          reference allocates (http.c:244-246, 270-272; the date
- *                          is the fixed 29 bytes the "37" there assumes)
- *   rhp_resp_tile_*_kernel reduce-then-scan over 4096-size tiles (tile sums in the
- *                          caller's work[], one workgroup scans those, every tile
- *                          is scanned in place): exclusive prefix sum -> out_off
- *   rhp_resp_write_kernel  wave per response: each segment copied 64 bytes per
- *                          store instruction in the reference's push order
- *                          (http_push_data / http_push_field, http.c:51-69); the
- *                          Content-Length digits as http_u32_sprint (:17-44) prints
- *                          them, one lane per digit
+ *   rhp_resp_tile_*_kernel every response's size, exactly the sum the reference
+ *                          allocates (http.c:244-246, 270-272; the date is the
+ *                          fixed 29 bytes the "37" there assumes), then a
+ *                          reduce-then-scan over 4096-size tiles (tile sums in
+ *                          the caller's work[], one workgroup scans those, every
+ *                          tile is scanned in place): exclusive prefix sum ->
+ *                          out_off
+ *   rhp_resp_write_kernel  wave per group of 64 consecutive responses: each lane
+ *                          assembles its response in the wave's LDS stage in the
+ *                          reference's push order (http_push_data /
+ *                          http_push_field, http.c:51-69; the Content-Length
+ *                          digits as http_u32_sprint, :17-44, prints them), then
+ *                          the wave stores the group's contiguous output with
+ *                          16-byte stores (the stage is shifted so LDS and HBM
+ *                          agree modulo 16; byte stores only at the group's two
+ *                          unaligned edges).  A group larger than the stage (big
+ *                          bodies) is written response by response, the wave's 64
+ *                          lanes copying each segment
  *
  * Byte copies are HBM-bound; the response bytes written are the algorithmic bytes.
  */
@@ -69,11 +76,6 @@ __device__ __forceinline__ uint64_t resp_size(const WParams &p, const rhp_resp_t
   return size;
 }
 
-__global__ __launch_bounds__(256) void rhp_resp_size_kernel(WParams p)
-{
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += gridDim.x * blockDim.x)
-    p.out_off[i + 1] = resp_size(p, p.resps[i]);
-}
 
 /* out_off[1..n] sizes -> out_off[0..n] offsets, reduce-then-scan over tiles of
  * kTile sizes: tile sums into work[], one workgroup scans work[] (exclusive),
@@ -107,12 +109,17 @@ __device__ __forceinline__ unsigned long long block_incl_scan(unsigned long long
   return v + (w ? part[w - 1] : 0);
 }
 
-__global__ __launch_bounds__(1024) void rhp_resp_tile_sum_kernel(const uint64_t *a, uint32_t n, uint64_t *work)
+/* sizes of a tile's responses into out_off[1..], and the tile's sum */
+__global__ __launch_bounds__(1024) void rhp_resp_tile_sum_kernel(WParams p, uint64_t *work)
 {
   __shared__ unsigned long long part[16];
-  const uint64_t lo = 1 + (uint64_t) blockIdx.x * kTile, hi = min(lo + kTile, (uint64_t) n + 1);
+  const uint64_t lo = 1 + (uint64_t) blockIdx.x * kTile, hi = min(lo + kTile, (uint64_t) p.n + 1);
   unsigned long long s = 0;
-  for (uint64_t k = lo + threadIdx.x; k < hi; k += 1024) s += a[k];
+  for (uint64_t k = lo + threadIdx.x; k < hi; k += 1024) {
+    const uint64_t z = resp_size(p, p.resps[k - 1]);
+    p.out_off[k] = z;
+    s += z;
+  }
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
   if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -156,10 +163,33 @@ __global__ __launch_bounds__(1024) void rhp_resp_tile_scan_kernel(uint64_t *a, u
   if (blockIdx.x == 0 && threadIdx.x == 0) a[0] = 0;
 }
 
-/* one segment of a response, 64 bytes per store instruction */
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+/* one segment of a response: bytes up to the first 16-aligned destination,
+ * then 16 bytes per lane (1 KiB per store instruction) from funnel-shifted
+ * aligned source dwords, then the tail bytes */
 __device__ __forceinline__ void put(uint8_t *dst, uint64_t &o, const uint8_t *src, uint32_t len, uint32_t lane)
 {
-  for (uint32_t j = lane; j < len; j += 64) dst[o + j] = src[j];
+  uint8_t *d = dst + o;
+  const uint32_t head = min(len, (uint32_t) ((16u - ((uintptr_t) d & 15u)) & 15u));
+  if (len < 128) {
+    for (uint32_t j = lane; j < len; j += 64) d[j] = src[j];
+    o += len;
+    return;
+  }
+  if (lane < head) d[lane] = src[lane];
+  const uint8_t *s = src + head;
+  const uint32_t body = (len - head) & ~15u;
+  const uintptr_t sa = (uintptr_t) s;
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t) 3);
+  const uint32_t sh = (uint32_t) sa & 3u, nd = (sh + (len - head) + 3u) >> 2;
+  for (uint32_t j = 16u * lane; j < body; j += 1024u) {
+    const uint32_t k = j >> 2;
+    const uint32_t w0 = w[k], w1 = w[k + 1], w2 = w[k + 2], w3 = w[k + 3], w4 = k + 4 < nd ? w[k + 4] : 0u;
+    *reinterpret_cast<u32x4 *>(d + head + j) = u32x4{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                                     __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+  }
+  for (uint32_t j = head + body + lane; j < len; j += 64) d[j] = src[j];
   o += len;
 }
 __device__ __forceinline__ void put_c(uint8_t *dst, uint64_t &o, const char *src, uint32_t len, uint32_t lane)
@@ -168,37 +198,131 @@ __device__ __forceinline__ void put_c(uint8_t *dst, uint64_t &o, const char *src
   o += len;
 }
 
+/* one response, wave-cooperatively (the path for groups larger than the stage) */
+__device__ void write_one(const WParams &p, uint32_t i, uint32_t lane)
+{
+  uint8_t *dst = p.out;
+  const rhp_resp_t r = p.resps[i];
+  uint64_t o = p.out_off[i];
+  put_c(dst, o, kHead, 9, lane);
+  put(dst, o, p.arena + r.status.off, r.status.len, lane);
+  put_c(dst, o, kServerDate, 19, lane);
+  if (lane < RHP_DATE_LEN) dst[o + lane] = (uint8_t) (p.date[lane >> 2] >> (8u * (lane & 3u)));
+  o += RHP_DATE_LEN;
+  put_c(dst, o, kType, 16, lane);
+  put(dst, o, p.arena + r.type.off, r.type.len, lane);
+  put_c(dst, o, kLength, 18, lane);
+  const uint32_t v = r.body.len, L = u32_len(v);   /* http_u32_sprint: most significant first */
+  if (lane < L) dst[o + lane] = (uint8_t) ('0' + (v / kPow10[L - 1u - lane]) % 10u);
+  o += L;
+  put_c(dst, o, kType, 2, lane);   /* CRLF */
+  for (uint32_t f = 0; f < r.fields_count; f++) {   /* http_push_field (http.c:61-69) */
+    const rhp_resp_field_t x = p.fields[r.fields_first + f];
+    put(dst, o, p.arena + x.name.off, x.name.len, lane);
+    if (lane < 2) dst[o + lane] = lane ? ' ' : ':';
+    o += 2;
+    put(dst, o, p.arena + x.value.off, x.value.len, lane);
+    put_c(dst, o, kType, 2, lane);
+  }
+  put_c(dst, o, kType, 2, lane);   /* the empty line */
+  put(dst, o, p.arena + r.body.off, r.body.len, lane);
+}
+
+/* ---- the lane-per-response stage writers (LDS byte o of the wave's stage) ---- */
+typedef __attribute__((address_space(3))) uint8_t lds8;
+
+/* a compile-time constant string */
+template <uint32_t N>
+__device__ __forceinline__ void st_const(lds8 *L, uint32_t &o, const char (&s)[N])
+{
+#pragma unroll
+  for (uint32_t j = 0; j + 1 < N; j++) L[o + j] = (uint8_t) s[j];
+  o += N - 1;
+}
+/* len bytes from global memory at src: the aligned dwords that hold them (no
+ * byte outside [src & ~3, src + len + 3) is read), funnel-shifted */
+__device__ __forceinline__ void st_span(lds8 *L, uint32_t &o, const uint8_t *src, uint32_t len)
+{
+  const uintptr_t a = (uintptr_t) src;
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t) 3);
+  const uint32_t sh = (uint32_t) a & 3u, nd = (sh + len + 3u) >> 2;
+  uint32_t lo = len ? w[0] : 0;
+  for (uint32_t j = 0; j < len; j += 4) {
+    const uint32_t k = (j >> 2) + 1u;
+    const uint32_t hi = k < nd ? w[k] : 0u;
+    const uint32_t d = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    L[o + j] = (uint8_t) d;
+    if (j + 1 < len) L[o + j + 1] = (uint8_t) (d >> 8);
+    if (j + 2 < len) L[o + j + 2] = (uint8_t) (d >> 16);
+    if (j + 3 < len) L[o + j + 3] = (uint8_t) (d >> 24);
+    lo = hi;
+  }
+  o += len;
+}
+
+constexpr uint32_t kStage = 16384;   /* LDS bytes per wave: groups up to 16 KiB - 16 */
+
 __global__ __launch_bounds__(256) void rhp_resp_write_kernel(WParams p)
 {
-  const uint32_t lane = threadIdx.x & 63u;
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[4 * kStage];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
   if (p.out_off[p.n] > p.out_size) return;   /* does not fit: sizes only (rhp.h) */
-  uint8_t *dst = p.out;
-  for (uint32_t i = wave; i < p.n; i += nwaves) {
-    const rhp_resp_t r = p.resps[i];
-    uint64_t o = p.out_off[i];
-    put_c(dst, o, kHead, 9, lane);
-    put(dst, o, p.arena + r.status.off, r.status.len, lane);
-    put_c(dst, o, kServerDate, 19, lane);
-    if (lane < RHP_DATE_LEN) dst[o + lane] = (uint8_t) (p.date[lane >> 2] >> (8u * (lane & 3u)));
-    o += RHP_DATE_LEN;
-    put_c(dst, o, kType, 16, lane);
-    put(dst, o, p.arena + r.type.off, r.type.len, lane);
-    put_c(dst, o, kLength, 18, lane);
-    const uint32_t v = r.body.len, L = u32_len(v);   /* http_u32_sprint: most significant first */
-    if (lane < L) dst[o + lane] = (uint8_t) ('0' + (v / kPow10[L - 1u - lane]) % 10u);
-    o += L;
-    put_c(dst, o, kType, 2, lane);   /* CRLF */
-    for (uint32_t f = 0; f < r.fields_count; f++) {   /* http_push_field (http.c:61-69) */
-      const rhp_resp_field_t x = p.fields[r.fields_first + f];
-      put(dst, o, p.arena + x.name.off, x.name.len, lane);
-      if (lane < 2) dst[o + lane] = lane ? ' ' : ':';
-      o += 2;
-      put(dst, o, p.arena + x.value.off, x.value.len, lane);
-      put_c(dst, o, kType, 2, lane);
+  lds8 *L = (lds8 *) (stage_all + wv * kStage);
+  const uint32_t groups = (p.n + 63u) / 64u;
+  for (uint32_t g = wave; g < groups; g += nwaves) {
+    const uint32_t i0 = g * 64u, i1 = min(i0 + 64u, p.n);
+    const uint64_t G0 = p.out_off[i0], G1 = p.out_off[i1];
+    const uint32_t shift = (uint32_t) (uintptr_t) (p.out + G0) & 15u;   /* LDS and HBM agree modulo 16 */
+    if (G1 - G0 + shift > kStage) {   /* big responses: the cooperative path */
+      for (uint32_t i = i0; i < i1; i++) write_one(p, i, lane);
+      continue;
     }
-    put_c(dst, o, kType, 2, lane);   /* the empty line */
-    put(dst, o, p.arena + r.body.off, r.body.len, lane);
+    const uint32_t i = i0 + lane;
+    if (i < i1) {
+      const rhp_resp_t r = p.resps[i];
+      uint32_t o = shift + (uint32_t) (p.out_off[i] - G0);
+      st_const(L, o, "HTTP/1.1 ");
+      st_span(L, o, p.arena + r.status.off, r.status.len);
+      st_const(L, o, "\r\nServer: *\r\nDate: ");
+#pragma unroll
+      for (uint32_t j = 0; j < RHP_DATE_LEN; j++) L[o + j] = (uint8_t) (p.date[j >> 2] >> (8u * (j & 3u)));
+      o += RHP_DATE_LEN;
+      st_const(L, o, "\r\nContent-Type: ");
+      st_span(L, o, p.arena + r.type.off, r.type.len);
+      st_const(L, o, "\r\nContent-Length: ");
+      const uint32_t v = r.body.len, D = u32_len(v);   /* http_u32_sprint: most significant first */
+      for (uint32_t j = 0; j < D; j++) L[o + j] = (uint8_t) ('0' + (v / kPow10[D - 1u - j]) % 10u);
+      o += D;
+      st_const(L, o, "\r\n");
+      for (uint32_t f = 0; f < r.fields_count; f++) {   /* http_push_field (http.c:61-69) */
+        const rhp_resp_field_t x = p.fields[r.fields_first + f];
+        st_span(L, o, p.arena + x.name.off, x.name.len);
+        st_const(L, o, ": ");
+        st_span(L, o, p.arena + x.value.off, x.value.len);
+        st_const(L, o, "\r\n");
+      }
+      st_const(L, o, "\r\n");   /* the empty line */
+      st_span(L, o, p.arena + r.body.off, r.body.len);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);   /* lgkmcnt(0): the stage is written (wave-local) */
+    __builtin_amdgcn_wave_barrier();
+    /* out[G0, G1) <- stage[shift, shift + G1 - G0): 16-byte stores between the
+     * first and the last 16-aligned addresses, byte stores outside */
+    const uint64_t A0 = G0 + ((16u - shift) & 15u), A1 = G1 - (((uint32_t) (uintptr_t) (p.out + G1)) & 15u);
+    if (A0 < A1) {
+      for (uint64_t a = A0 + 16u * lane; a < A1; a += 1024u) {
+        const uint32_t so = (uint32_t) (a - G0) + shift;
+        const u32x4 d = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(L + so);
+        *reinterpret_cast<u32x4 *>(p.out + a) = d;
+      }
+      if (lane < A0 - G0) p.out[G0 + lane] = L[shift + lane];
+      if (lane < G1 - A1) p.out[A1 + lane] = L[shift + (uint32_t) (A1 - G0) + lane];
+    } else {   /* the whole group within one 16-byte line (or two) */
+      for (uint32_t j = lane; j < G1 - G0; j += 64) p.out[G0 + j] = L[shift + j];
+    }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -232,16 +356,13 @@ extern "C" int rhp_write_responses(const rhp_resp_batch_t *b, void *stream)
   memcpy(p.date, b->date, RHP_DATE_LEN);
   if (b->n == 0) return (int) hipMemsetAsync(b->out_off, 0, sizeof(uint64_t), s);
   const uint32_t cap = (uint32_t) g_writer_cus * 8u;
-  uint32_t g1 = (b->n + 255u) / 256u;
-  if (g1 > cap) g1 = cap;
-  hipLaunchKernelGGL(rhp_resp_size_kernel, dim3(g1), dim3(256), 0, s, p);
   const uint32_t tiles = (b->n + kTile - 1u) / kTile;
-  hipLaunchKernelGGL(rhp_resp_tile_sum_kernel, dim3(tiles), dim3(1024), 0, s, b->out_off, b->n, b->work);
+  hipLaunchKernelGGL(rhp_resp_tile_sum_kernel, dim3(tiles), dim3(1024), 0, s, p, b->work);
   hipLaunchKernelGGL(rhp_resp_top_scan_kernel, dim3(1), dim3(1024), 0, s, b->work, tiles);
   hipLaunchKernelGGL(rhp_resp_tile_scan_kernel, dim3(tiles), dim3(1024), 0, s, b->out_off, b->n,
                      (const uint64_t *) b->work);
-  uint32_t g3 = (b->n + 3u) / 4u;   /* 4 waves per workgroup, a wave per response */
-  if (g3 > cap * 4u) g3 = cap * 4u;
+  uint32_t g3 = (b->n + 255u) / 256u;   /* 4 waves per workgroup, a wave per 64 responses */
+  if (g3 > cap) g3 = cap;
   hipLaunchKernelGGL(rhp_resp_write_kernel, dim3(g3), dim3(256), 0, s, p);
   return (int) hipGetLastError();
 }

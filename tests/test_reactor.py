@@ -67,19 +67,22 @@ def test_server_cases_host_parser():
     assert "config1 16 pipelined   responses 16  callbacks 16" in out
 
 
-def test_server_cases_host_async_parser():
+@pytest.mark.parametrize("writer", ["host", "host-batch"])
+def test_server_cases_host_async_parser(writer, monkeypatch):
     """Asynchronous rounds (batch.c "host-async": the gpu mode's slots and
-    eventfd completion, parsed on a worker thread): the same cases."""
+    eventfd completion, parsed on a worker thread), replies written at once or
+    batched per round: the same cases."""
+    monkeypatch.setenv("RHP_REACTOR_WRITER", writer)
     out = _run([os.path.join(BIN, "server_test"), "32", "64"], "host-async")
     assert "parser: host-async" in out and "OK (0 failures)" in out
     assert "config1 16 pipelined   responses 16  callbacks 16" in out
 
 
-def _burst(parser, conns=64, pipelined=64, reps=5):
+def _burst(parser, conns=64, pipelined=64, reps=5, writer="host"):
     """burst_test: conns x pipelined requests land before the loop starts, so
     rounds hold conns x pipelined requests; req/s per burst (the first burst,
     which pays first-use costs, is dropped)."""
-    env = dict(os.environ, RHP_REACTOR_PARSER=parser, RHP_REACTOR_STATS="1")
+    env = dict(os.environ, RHP_REACTOR_PARSER=parser, RHP_REACTOR_STATS="1", RHP_REACTOR_WRITER=writer)
     p = subprocess.run([os.path.join(BIN, "burst_test"), str(conns), str(pipelined), str(reps)], env=env,
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0 and "OK (0 failures)" in p.stdout, p.stdout + p.stderr
@@ -100,16 +103,22 @@ def test_burst_rounds_gpu_vs_host():
     MI355X parser (asynchronous rounds) against the host parser, same process
     layout; both numbers are printed and recorded in DESIGN.md."""
     gpu, gpu_round, out_g = _burst("gpu")
+    gpu_w, _, out_w = _burst("gpu", writer="gpu")
     host, host_round, out_h = _burst("host")
-    print(f"burst req/s: gpu {gpu:.0f} ({gpu_round:.0f} requests/round), host {host:.0f} ({host_round:.0f})")
-    print(out_g, out_h)
+    print(f"burst req/s: gpu {gpu:.0f} ({gpu_round:.0f} requests/round), gpu parser + gpu writer {gpu_w:.0f}, "
+          f"host {host:.0f} ({host_round:.0f})")
+    print(out_g, out_w, out_h)
     assert gpu_round >= 4000 and host_round >= 4000
     assert gpu >= 0.8 * host, (gpu, host)
 
 
 @pytest.mark.gpu
-def test_server_cases_gpu_batch_parser():
-    """The same cases with sessions parsed by rhp_parse_batch on the MI355X."""
+@pytest.mark.parametrize("writer", ["host", "gpu"])
+def test_server_cases_gpu_batch_parser(writer, monkeypatch):
+    """The same cases with sessions parsed by rhp_parse_batch on the MI355X
+    (asynchronous rounds), replies written at once or by rhp_write_responses
+    once per round."""
+    monkeypatch.setenv("RHP_REACTOR_WRITER", writer)
     out = _run([os.path.join(BIN, "server_test"), "64", "64"], "gpu")
     print(out)
     assert "parser: gpu" in out and "OK (0 failures)" in out

@@ -98,10 +98,11 @@ def decode_echoes(raw: bytes):
     return out
 
 
-def run_echo(tmp_path, stream: bytes, chunk: int, parser: str):
+def run_echo(tmp_path, stream: bytes, chunk: int, parser: str, writer: str = "host"):
     src, dst = tmp_path / "in.bin", tmp_path / "out.bin"
     src.write_bytes(stream)
-    p = subprocess.run([ECHO, str(src), str(chunk), str(dst)], env=dict(os.environ, RHP_REACTOR_PARSER=parser),
+    p = subprocess.run([ECHO, str(src), str(chunk), str(dst)],
+                       env=dict(os.environ, RHP_REACTOR_PARSER=parser, RHP_REACTOR_WRITER=writer),
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and "OK" in p.stdout, p.stdout + p.stderr
     assert f"parser: {parser}" in p.stdout
@@ -112,17 +113,20 @@ CASES = [("mixed", stream_mixed, 1 << 20), ("mixed", stream_mixed, 1000), ("mixe
          ("mixed", stream_mixed, 7), ("bad", stream_bad, 1 << 20), ("bad", stream_bad, 50)]
 
 
-@pytest.mark.parametrize("parser", ["host", "host-async"])
+@pytest.mark.parametrize("parser,writer", [("host", "host"), ("host-async", "host"), ("host-async", "host-batch")])
 @pytest.mark.parametrize("name,make,chunk", CASES)
-def test_server_records_match_oracle_sequential_loop(tmp_path, name, make, chunk, parser):
+def test_server_records_match_oracle_sequential_loop(tmp_path, name, make, chunk, parser, writer):
     s = make()
     want = oracle_sequential(s)
     assert len(want) >= 3
-    assert run_echo(tmp_path, s, chunk, parser) == want
+    assert run_echo(tmp_path, s, chunk, parser, writer) == want
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("writer", ["host", "gpu"])
 @pytest.mark.parametrize("name,make,chunk", CASES)
-def test_server_records_gpu_match_oracle_sequential_loop(tmp_path, name, make, chunk):
+def test_server_records_gpu_match_oracle_sequential_loop(tmp_path, name, make, chunk, writer):
+    """GPU parser (asynchronous rounds); replies written by the host as the
+    reference does, or by rhp_write_responses once per round."""
     s = make()
-    assert run_echo(tmp_path, s, chunk, "gpu") == oracle_sequential(s)
+    assert run_echo(tmp_path, s, chunk, "gpu", writer) == oracle_sequential(s)

@@ -7,7 +7,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import libreactorng_amd as rhp
-SLOTS = 12
+SLOTS = 16
 lib = rhp.lib()
 lib.rhp_debug_stamps.argtypes = [ctypes.c_void_p]
 names = ["A wait window", "C-E switch/refill/issue", "decode", "walk", "finalize/handover"]
@@ -58,4 +58,7 @@ for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, 1), (r
     nw_, ni_ = st[used, 10], st[used, 11]
     print("   by wave slot: lane occupancy (walked / (walked + idle))")
     print("     " + " ".join(f"{nw_[idx == k].sum() / (nw_[idx == k].sum() + ni_[idx == k].sum()):5.2f}" for k in range(16)))
+    il, dry = st[used, 12], st[used, 13]
+    print(f"   idle lane-iterations: {ni_.sum():.0f}, of them while the pool had requests {il.sum():.0f}; "
+          f"iterations after the pool ran dry: {dry.mean():.1f} per wave (of {st[used, 5].mean():.1f})")
     print(f"   workgroups: last wave's loop end {q(ends)}; first wave's {q(firsts)}", flush=True)

@@ -74,7 +74,10 @@ enum : uint32_t {
   kStageWave = 64 * kBlock,                      /* one window per lane */
   kPark = 0,                                     /* the DONE index: idle lanes step here */
   kDeferExact = 0x8000u,                         /* reqs[i].flags while deferred (kernel-internal) */
-  kDeferFrame = 0x4000u,
+  /* http mode: the replay's instructions, in the body_kind word of the hint
+   * finalize leaves in http[i] (ret in the low 16 bits) */
+  kHintExact = 0x40000000u,
+  kHintFrame = 0x80000000u,
   /* workgroup pool area after the staging buffers: counters, then the long-
    * request bitmap (ranges up to kOrderSpan requests) and list */
   kPoolWords = 8,                                /* counter, replay flag, list length, list cursor */
@@ -108,8 +111,10 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
  * own (never read by the kernel): slots 0-4 section cycles, 5 iterations,
  * 6 entry, 7 loop start, 8 loop end, 9 exit, 10 lane-windows walked,
  * 11 lane-iterations without a window to walk, 12 of them while the pool
- * still had requests, 13 iterations after the pool ran dry */
-enum : uint32_t { kStampSlots = 16 };
+ * still had requests, 13 iterations after the pool ran dry, 14 the replay's
+ * start (after the workgroup barrier), 15 / 16 the wave's shader cycles in the
+ * replay's exact path / framing, 17 exact requests, 18 framed requests */
+enum : uint32_t { kStampSlots = 20 };
 __device__ unsigned long long g_stamps[8192 * kStampSlots];
 #define RHP_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); (t) = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0); } while (0)
@@ -220,10 +225,10 @@ __device__ __forceinline__ uint64_t strtoull10_gpu(const uint8_t *s, uint32_t n)
  * that is Content-Length or neither; anything else takes http_frame.  Reads no
  * header record and no method byte: on batches larger than the caches those
  * re-reads are HBM traffic. */
-__device__ __forceinline__ bool http_frame_fast(const uint8_t *b, uint64_t len, const rhp_req_t &r, rhp_http_t *x,
+__device__ __forceinline__ bool http_frame_fast(const uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x,
                                                 uint32_t cand, uint32_t crec_lo, uint32_t crec_hi)
 {
-  const int64_t n = r.ret;
+  const int64_t n = ret;
   rhp_http_t o = {1, 0, (uint64_t) n, 0};
   const uint32_t hdr = cand & 0x3fffffffu;
   if (!(cand & 0x40000000u) && hdr != 0) {   /* not GET (http.c:198-202), some candidate */
@@ -245,12 +250,14 @@ __device__ __forceinline__ bool http_frame_fast(const uint8_t *b, uint64_t len, 
   return true;
 }
 
-/* http_read_request framing of a request the DFA parsed (http mode only) */
-__device__ __forceinline__ void finish_http(const Params &p, uint32_t i, uint64_t off, uint64_t len, rhp_req_t r,
+/* http_read_request framing of a request the DFA parsed (http mode only;
+ * its request record is final, only the general path reads it) */
+__device__ __forceinline__ void finish_http(const Params &p, uint32_t i, uint64_t off, uint64_t len, int32_t ret,
                                             uint32_t cand, uint32_t crec_lo, uint32_t crec_hi)
 {
+  if (http_frame_fast(p.bytes_rw + off, len, ret, &p.http[i], cand, crec_lo, crec_hi)) return;
   const rhp_hdr_t *h = p.hdrs + (uint64_t) i * p.hs_req;
-  if (http_frame_fast(p.bytes_rw + off, len, r, &p.http[i], cand, crec_lo, crec_hi)) return;
+  const rhp_req_t r = p.reqs[i];
   http_frame(p.bytes_rw + off, len, r, h, p.hs_hdr, &p.http[i], (cand >> 31) ? ~0ull : (uint64_t) (cand & 0x3fffffffu));
 }
 
@@ -641,12 +648,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       r.path_len = (uint16_t) (rl >> 16);
       r.minor_version = (int8_t) ((kn >> 3) & 1u);
       r.num_headers = (uint16_t) nh;
-      r.flags = http ? (uint16_t) kDeferFrame : (uint16_t) 0;   /* framing: replay */
-      if (http) {
+      if (http) {   /* framing: replay, from the hints left in the record it will overwrite */
         *wg_deferred = 1u;
-        /* framing hints for the replay, in the record it will overwrite */
         typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-        *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{cand, 0u, crec_lo, crec_hi};
+        *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{cand, kHintFrame | (term_pos + 1u), crec_lo, crec_hi};
       }
     } else if (bad) {
       r.ret = -1;
@@ -654,6 +659,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     } else {
       r.flags = (uint16_t) kDeferExact;   /* exact path: replay */
       *wg_deferred = 1u;
+      if (http) {
+        typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+        *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{0u, kHintExact, 0u, 0u};
+      }
     }
     store_req(p.reqs + dcur, r);
     dhas = false;
@@ -908,28 +917,52 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * finalize deferred: the exact scalar path, and http_read_request framing of
    * DFA-parsed requests in http mode.  Nothing to do -> no pass at all. */
   __syncthreads();
+#ifdef RHP_STAMPS
+  if (lane == 0) g_stamps[((blockIdx.x * WAVES + (tid >> 6)) % 8192) * kStampSlots + 14] = __builtin_amdgcn_s_memrealtime();
+  unsigned long long rp[4] = {0, 0, 0, 0};
+#endif
   if (*wg_deferred) {
+    typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
     for (uint32_t i = wg_lo + tid; i < wg_hi; i += WAVES * 64) {
-      /* everything a request needs first, in one round trip */
-      rhp_req_t r;
-      const u32x4 rv = *GLOBAL(const u32x4, p.reqs + i);
-      __builtin_memcpy(&r, &rv, sizeof r);
+      /* what a request needs first, in one round trip: in http mode the hint
+       * left in its http record says what to do (and holds ret), so neither
+       * the request record is read nor its flags written back */
       const uint64_t off = p.offsets[i], end = p.offsets[i + 1];
-      typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-      const u32x4a4 hint = http ? *GLOBAL(const u32x4a4, &p.http[i]) : u32x4a4{0u, 0u, 0u, 0u};
-      const uint32_t f = r.flags;
-      if (!(f & (kDeferExact | kDeferFrame))) continue;
-      if (f & kDeferExact) {
-        finish_exact(p, i, off, end - off);
+      uint32_t f = 0, ret = 0;
+      u32x4a4 hint = u32x4a4{0u, 0u, 0u, 0u};
+      if (http) {
+        hint = *GLOBAL(const u32x4a4, &p.http[i]);
+        f = hint[1] & (kHintExact | kHintFrame);
+        ret = hint[1] & 0xffffu;
       } else {
-        r.flags = 0;
-        finish_http(p, i, off, end - off, r, hint[0], hint[2], hint[3]);
-        p.reqs[i].flags = 0;
+        f = (p.reqs[i].flags & kDeferExact) ? kHintExact : 0u;
       }
+      if (!f) continue;
+#ifdef RHP_STAMPS
+      unsigned long long c0 = 0, c1 = 0;
+      RHP_STAMP(c0);
+#endif
+      if (f & kHintExact) finish_exact(p, i, off, end - off);
+#ifdef RHP_STAMPS
+      RHP_STAMP(c1);
+      rp[0] += c1 - c0;
+      rp[2] += __popcll(__builtin_amdgcn_ballot_w64((f & kHintExact) != 0));
+      c0 = c1;
+#endif
+      if (f & kHintFrame) finish_http(p, i, off, end - off, (int32_t) ret, hint[0], hint[2], hint[3]);
+#ifdef RHP_STAMPS
+      RHP_STAMP(c1);
+      rp[1] += c1 - c0;
+      rp[3] += __popcll(__builtin_amdgcn_ballot_w64((f & kHintFrame) != 0));
+#endif
     }
   }
 #ifdef RHP_STAMPS
-  if (lane == 0) g_stamps[((blockIdx.x * WAVES + (tid >> 6)) % 8192) * kStampSlots + 9] = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0) {
+    const uint32_t w = (blockIdx.x * WAVES + (tid >> 6)) % 8192;
+    g_stamps[w * kStampSlots + 9] = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < 4; k++) g_stamps[w * kStampSlots + 15 + k] = rp[k];
+  }
 #endif
 }
 

@@ -7,7 +7,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import libreactorng_amd as rhp
-SLOTS = 16
+SLOTS = 20
 lib = rhp.lib()
 lib.rhp_debug_stamps.argtypes = [ctypes.c_void_p]
 names = ["A wait window", "C-E switch/refill/issue", "decode", "walk", "finalize/handover"]
@@ -37,7 +37,7 @@ for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, 1), (r
         print(f"   {names[k]:26s} {tot[k] / it:8.0f}  ({100 * tot[k] / tot.sum():.1f} %)")
     loop = st[used, :5].sum(axis=1)
     print(f"   per wave: {loop.mean():.0f} cycles in the loop (min {loop.min():.0f}, max {loop.max():.0f})")
-    rt = st[used, 6:10] * 10.0 / 1000.0   # us
+    rt = np.concatenate([st[used, 6:10], st[used, 14:15]], axis=1) * 10.0 / 1000.0   # us
     t0 = rt[:, 0].min()
     rt = rt - t0
     q = lambda v: f"{np.percentile(v, 0):6.1f} {np.percentile(v, 50):6.1f} {np.percentile(v, 99):6.1f} {v.max():6.1f}"
@@ -45,7 +45,7 @@ for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, 1), (r
     print(f"     entry       {q(rt[:, 0])}")
     print(f"     loop start  {q(rt[:, 1])}   prologue {q(rt[:, 1] - rt[:, 0])}")
     print(f"     loop end    {q(rt[:, 2])}   loop     {q(rt[:, 2] - rt[:, 1])}")
-    print(f"     exit        {q(rt[:, 3])}   replay   {q(rt[:, 3] - rt[:, 2])}")
+    print(f"     exit        {q(rt[:, 3])}   barrier  {q(rt[:, 4] - rt[:, 2])}   replay {q(rt[:, 3] - rt[:, 4])}")
     # by wave slot in the workgroup (dispatch age): iterations and loop end
     idx = np.nonzero(used)[0] % 16
     its = st[used, 5]
@@ -61,4 +61,7 @@ for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, 1), (r
     il, dry = st[used, 12], st[used, 13]
     print(f"   idle lane-iterations: {ni_.sum():.0f}, of them while the pool had requests {il.sum():.0f}; "
           f"iterations after the pool ran dry: {dry.mean():.1f} per wave (of {st[used, 5].mean():.1f})")
+    rx = st[used, 15:19]
+    print(f"   replay per wave: exact path {rx[:, 0].mean():.0f} cycles ({rx[:, 2].mean():.1f} requests), "
+          f"framing {rx[:, 1].mean():.0f} cycles ({rx[:, 3].mean():.1f} requests)")
     print(f"   workgroups: last wave's loop end {q(ends)}; first wave's {q(firsts)}", flush=True)

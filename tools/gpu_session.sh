@@ -3,11 +3,11 @@
 # bench line, rocprofv3 kernel-trace summaries of configs 2/3/5 and PMC
 # FETCH_SIZE / WRITE_SIZE passes (separate runs).  Every GPU step has its own
 # time limit; steps are chained with && so a failure stops the session.
-# STEPS=tests,bench,prof,pmc (default all)
+# STEPS=tests,bench,prof,pmc,sq,writer,smoke (default all)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out && export TMPDIR=/tmp
 TAG=${TAG:-s}
-STEPS=${STEPS:-tests,bench,prof,pmc}
+STEPS=${STEPS:-tests,bench,prof,pmc,sq,writer,smoke}
 has() { [[ ",$STEPS," == *",$1,"* ]]; }
 ok=0
 step_tests() {
@@ -36,5 +36,17 @@ step_pmc() {
     echo PMC_${c}_OK
   done
 }
+step_sq() {
+  TAG=sq_${TAG} CONFIG=get256 bash tools/pmc_sq.sh > gpurun_out/sq_${TAG}.txt 2>&1 && echo SQ_OK
+}
+step_writer() {
+  timeout -k 10 120 python3 tools/bench_writer.py > gpurun_out/writer_${TAG}.json 2>&1 \
+    && timeout -k 10 180 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_${TAG}_writer -o run \
+      -- python3 tools/bench_writer.py > gpurun_out/prof_${TAG}_writer.log 2>&1 && echo WRITER_OK
+}
+step_smoke() {
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" > gpurun_out/smoke_${TAG}.log 2>&1 \
+    && tail -1 gpurun_out/smoke_${TAG}.log
+}
 ( ! has tests || step_tests ) && ( ! has bench || step_bench ) && ( ! has prof || step_prof ) && ( ! has pmc || step_pmc ) \
-  && echo SESSION_OK
+  && ( ! has sq || step_sq ) && ( ! has writer || step_writer ) && ( ! has smoke || step_smoke ) && echo SESSION_OK

@@ -387,6 +387,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   const uint64_t o_lo = pool_dry ? 0 : p.offsets[wg_lo], o_hi = pool_dry ? 0 : p.offsets[wg_hi];
   const uint64_t base = o_lo & ~(uint64_t) 3;
   const uint8_t *wbytes = p.bytes + base;
+  /* the range's bytes as a raw buffer: window loads take 32-bit offsets from
+   * base (a batch is below 4 GiB), no 64-bit address per load */
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(wbytes), 0, -1, 0x00020000);
 
   /* ---- walk state (the request whose window landed) ---- */
   uint32_t st = kPark;                 /* table index (rhp_dfa.h idx2) */
@@ -400,7 +403,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   uint32_t nw = 0;                     /* next window: byte offset from base | kind (0 none, 1
                                           continuation, 2 first window of pend); windows are 4-aligned */
   u32x4 W[kParts];                     /* the window in registers */
-  const uint32_t stage = kLdsTable + (tid >> 6) * kStageWave;
+  const uint32_t stage = __builtin_amdgcn_readfirstlane(kLdsTable + (tid >> 6) * kStageWave);   /* wave-uniform */
 
   /* ---- decode state (the request whose previous window is decoded) ----
    *   kn   request-line events consumed (0 ME, 1 PE, 2 RL, 3 done) | minor << 3
@@ -639,32 +642,28 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     if (!fin) return false;
     const bool ok = !ovfl && is_done2(e) && term_pos < dlen && term_pos < RHP_MAX_LEN;
     const bool bad = ovfl ? ovf - 1u < dlen : (is_err2(e) && term_pos < dlen);
-    rhp_req_t r = {};
-    r.minor_version = -1;
+    /* the record as four dwords (rhp.h rhp_req_t: ret; method_len, path_off;
+     * path_len, method_off 0, minor_version; num_headers, flags) */
+    u32x4 rq = u32x4{0u, 0u, 0xff000000u, 0u};   /* minor_version -1 */
     if (ok) {
-      r.ret = (int32_t) term_pos + 1;
-      r.method_len = (uint16_t) rl;
-      r.path_off = (uint16_t) (rl + 1u);
-      r.path_len = (uint16_t) (rl >> 16);
-      r.minor_version = (int8_t) ((kn >> 3) & 1u);
-      r.num_headers = (uint16_t) nh;
+      rq = u32x4{term_pos + 1u, (rl & 0xffffu) | ((rl + 1u) << 16), (rl >> 16) | (((kn >> 3) & 1u) << 24), nh};
       if (http) {   /* framing: replay, from the hints left in the record it will overwrite */
         *wg_deferred = 1u;
         typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
         *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{cand, kHintFrame | (term_pos + 1u), crec_lo, crec_hi};
       }
     } else if (bad) {
-      r.ret = -1;
+      rq[0] = 0xffffffffu;   /* -1 */
       if (http) store_http_bad(p.http + dcur);
     } else {
-      r.flags = (uint16_t) kDeferExact;   /* exact path: replay */
+      rq[3] = (uint32_t) kDeferExact << 16;   /* exact path: replay */
       *wg_deferred = 1u;
       if (http) {
         typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
         *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{0u, kHintExact, 0u, 0u};
       }
     }
-    store_req(p.reqs + dcur, r);
+    *GLOBAL(u32x4, p.reqs + dcur) = rq;
     dhas = false;
     return true;
   };
@@ -736,8 +735,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #define RHP_ISSUE_LOADS(AUX)                                                                             \
     _Pragma("unroll") for (int i = 0; i < (int) kParts; i++) {                                           \
       const uint32_t part = dma_part(dma_window((uint32_t) i, lane), lane);                              \
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(wbytes + a[i] + 16u * part),       \
-          (__attribute__((address_space(3))) void *) (lds + stage + 1024u * i), 16, 0, AUX);             \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc,                                                    \
+          (__attribute__((address_space(3))) void *) (lds + stage + 1024u * i), 16, a[i] + 16u * part,   \
+          0, 0, AUX);                                                                                    \
     }
     if (nt) { RHP_ISSUE_LOADS(2) } else { RHP_ISSUE_LOADS(0) }
 #undef RHP_ISSUE_LOADS

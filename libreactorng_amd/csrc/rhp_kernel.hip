@@ -541,9 +541,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         const uint32_t e = base + (uint32_t) __builtin_ctz(eolm | 0x80000000u);
         const uint32_t co = t ? pco : base + (uint32_t) __builtin_ctz(com | 0x80000000u);
         const uint32_t lo = ls | ((co - ls) << 16), hi = (co + 2u) | ((e - co - 3u) << 16);
-#ifndef RHP_EXP_NOSTORE   /* timing experiment: header records computed, not stored */
         store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi});
-#endif
         if (http) {   /* uniform: framing candidates only in http mode */
           const uint32_t nlen = co - ls;
           const bool cnd = has && (nlen == 14u || nlen == 17u);
@@ -575,9 +573,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const bool rec = has && !stop;
       const uint32_t lo = ls | ((co - ls) << 16), hi = (co + 2u) | ((e - co - 3u) << 16);
       const uint64_t st_m = __builtin_amdgcn_ballot_w64(rec);
-#ifndef RHP_EXP_NOSTORE
       if (st_m) store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi});
-#endif
       if (http) {
         const uint32_t nlen = co - ls;
         const bool cnd = rec && (nlen == 14u || nlen == 17u);
@@ -821,9 +817,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #endif
     /* [F] walk + decode of the previous window */
     decode_begin();
-#if !defined(RHP_EXP_NODECODE) && !defined(RHP_DECODE_AFTER)
     if (__builtin_amdgcn_ballot_w64(dhas)) decode_window();
-#endif
 #pragma unroll
     for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
 #ifdef RHP_STAMPS
@@ -845,9 +839,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #ifdef RHP_STAMPS
     wait_lgkm0();
     RHP_STAMP(t1); acc[3] += t1 - t0; t0 = t1;
-#endif
-#ifdef RHP_DECODE_AFTER
-    if (any_dec) decode_window();
 #endif
     /* [G] */
     const bool done = any_dec ? decode_end() : false;
@@ -872,19 +863,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       dhas = false;
     }
     wpos += (int32_t) kBlock;
-#ifdef RHP_EXP_PAD   /* timing experiment: RHP_EXP_PAD independent VALU per iteration (4 chains) */
-    {
-      uint32_t x0 = lane, x1 = lane + 1u, x2 = lane + 2u, x3 = lane + 3u;
-#pragma unroll
-      for (int k = 0; k < RHP_EXP_PAD / 4; k++) {
-        asm volatile("v_add_u32 %0, %0, 1" : "+v"(x0));
-        asm volatile("v_add_u32 %0, %0, 1" : "+v"(x1));
-        asm volatile("v_add_u32 %0, %0, 1" : "+v"(x2));
-        asm volatile("v_add_u32 %0, %0, 1" : "+v"(x3));
-      }
-      asm volatile("" :: "v"(x0), "v"(x1), "v"(x2), "v"(x3));
-    }
-#endif
 #ifdef RHP_STAMPS
     RHP_STAMP(t1); acc[4] += t1 - t0; acc[5] += 1;
 #endif

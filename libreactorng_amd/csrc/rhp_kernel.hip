@@ -113,7 +113,8 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
  * 11 lane-iterations without a window to walk, 12 of them while the pool
  * still had requests, 13 iterations after the pool ran dry, 14 the replay's
  * start (after the workgroup barrier), 15 / 16 the wave's shader cycles in the
- * replay's exact path / framing, 17 exact requests, 18 framed requests */
+ * replay's pass 2 (listed scalar paths) / pass 1, 17 requests it ran in pass 2,
+ * 18 requests it framed in pass 1 */
 enum : uint32_t { kStampSlots = 20 };
 __device__ unsigned long long g_stamps[8192 * kStampSlots];
 #define RHP_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); (t) = __builtin_amdgcn_s_memtime(); \
@@ -188,29 +189,25 @@ __device__ __forceinline__ void load28(const uint8_t *b, uint32_t (&d)[7])
 /* byte j of a dword array (j constant after unrolling) */
 #define RHP_BYTE(d, j) (((d)[(j) >> 2] >> (8 * ((j) & 3))) & 0xffu)
 
-/* Case-insensitive compare of a parsed header name with a lower-case literal
- * of n <= 28 bytes: OR 0x20 folds letters; the one non-letter, '-', could only
- * collide with CR, which a parsed name cannot hold (tchar only) */
+/* Case-insensitive compare of the first n <= 28 bytes of d (a header name
+ * already in registers) with a lower-case literal: OR 0x20 folds letters; the
+ * one non-letter, '-', could only collide with CR, which a parsed name cannot
+ * hold (tchar only) */
 template <uint32_t N>
-__device__ __forceinline__ bool name_is(const uint8_t *b, const rhp_hdr_t &h, const char (&lit)[N])
+__device__ __forceinline__ bool name_is(const uint32_t (&d)[7], const char (&lit)[N])
 {
   constexpr uint32_t n = N - 1;
-  if (h.name_off == RHP_NAME_NULL || h.name_len != n) return false;
-  uint32_t d[7];
-  load28(b + h.name_off, d);
   uint32_t diff = 0;
 #pragma unroll
   for (uint32_t j = 0; j < n; j++) diff |= (RHP_BYTE(d, j) | 0x20u) ^ (uint32_t) lit[j];
   return diff == 0;
 }
 
-/* strtoull over a header value of n bytes (rhp_scalar.h strtoull10) from a
- * 28-byte register window; the byte walk continues past it only for longer
- * values */
-__device__ __forceinline__ uint64_t strtoull10_gpu(const uint8_t *s, uint32_t n)
+/* strtoull over a header value of n bytes at s (rhp_scalar.h strtoull10), its
+ * first 28 bytes already in d; the byte walk continues past them only for
+ * longer values */
+__device__ __forceinline__ uint64_t strtoull10_gpu(const uint8_t *s, const uint32_t (&d)[7], uint32_t n)
 {
-  uint32_t d[7];
-  load28(s, d);
   uint32_t st = 0;
   bool neg = false, ovf = false;
   uint64_t v = 0;
@@ -224,7 +221,8 @@ __device__ __forceinline__ uint64_t strtoull10_gpu(const uint8_t *s, uint32_t n)
  * hints (cand, crec: see the decode state) -- GET, no candidate header, or one
  * that is Content-Length or neither; anything else takes http_frame.  Reads no
  * header record and no method byte: on batches larger than the caches those
- * re-reads are HBM traffic. */
+ * re-reads are HBM traffic.  The candidate's name and value are loaded
+ * together, one memory round trip. */
 __device__ __forceinline__ bool http_frame_fast(const uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x,
                                                 uint32_t cand, uint32_t crec_lo, uint32_t crec_hi)
 {
@@ -233,12 +231,15 @@ __device__ __forceinline__ bool http_frame_fast(const uint8_t *b, uint64_t len, 
   const uint32_t hdr = cand & 0x3fffffffu;
   if (!(cand & 0x40000000u) && hdr != 0) {   /* not GET (http.c:198-202), some candidate */
     if ((cand >> 31) || (hdr & (hdr - 1)) != 0) return false;
-    rhp_hdr_t hc;
-    hc.name_off = (uint16_t) crec_lo; hc.name_len = (uint16_t) (crec_lo >> 16);
-    hc.value_off = (uint16_t) crec_hi; hc.value_len = (uint16_t) (crec_hi >> 16);
-    if (name_is(b, hc, "transfer-encoding")) return false;   /* chunked framing: the general path */
-    if (name_is(b, hc, "content-length") && hc.value_len != 0) {
-      const uint64_t size = strtoull10_gpu(b + hc.value_off, hc.value_len);
+    /* a candidate's name is never RHP_NAME_NULL (its length is 14 or 17) */
+    const uint32_t name_off = crec_lo & 0xffffu, name_len = crec_lo >> 16;
+    const uint32_t value_off = crec_hi & 0xffffu, value_len = crec_hi >> 16;
+    uint32_t dn[7], dv[7];
+    load28(b + name_off, dn);
+    load28(b + value_off, dv);
+    if (name_len == 17u && name_is(dn, "transfer-encoding")) return false;   /* chunked framing: the general path */
+    if (name_len == 14u && name_is(dn, "content-length") && value_len != 0) {
+      const uint64_t size = strtoull10_gpu(b + value_off, dv, value_len);
       if (len < (uint64_t) n + size) {
         o.result = 0; o.consumed = 0;
       } else {
@@ -248,17 +249,6 @@ __device__ __forceinline__ bool http_frame_fast(const uint8_t *b, uint64_t len, 
   }
   *x = o;
   return true;
-}
-
-/* http_read_request framing of a request the DFA parsed (http mode only;
- * its request record is final, only the general path reads it) */
-__device__ __forceinline__ void finish_http(const Params &p, uint32_t i, uint64_t off, uint64_t len, int32_t ret,
-                                            uint32_t cand, uint32_t crec_lo, uint32_t crec_hi)
-{
-  if (http_frame_fast(p.bytes_rw + off, len, ret, &p.http[i], cand, crec_lo, crec_hi)) return;
-  const rhp_hdr_t *h = p.hdrs + (uint64_t) i * p.hs_req;
-  const rhp_req_t r = p.reqs[i];
-  http_frame(p.bytes_rw + off, len, r, h, p.hs_hdr, &p.http[i], (cand >> 31) ? ~0ull : (uint64_t) (cand & 0x3fffffffu));
 }
 
 /* Params pointers are generic in the kernel's view (they sit in a struct);
@@ -891,9 +881,15 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 
   /* Replay: the rare paths run here, after the DFA loop, so none of their
    * registers are live in it.  Once every wave of the workgroup is done, the
-   * workgroup walks its range, one request per thread, and finishes what
-   * finalize deferred: the exact scalar path, and http_read_request framing of
-   * DFA-parsed requests in http mode.  Nothing to do -> no pass at all. */
+   * workgroup finishes what finalize deferred, in two passes over its range:
+   * (1) one request per thread, http_read_request framing of the DFA-parsed
+   * requests from the decode's hints (no dependent loads), listing in LDS the
+   * requests that need a serial scalar path -- the exact parse, general
+   * framing; (2) the listed requests, one per thread.  A scalar path takes
+   * many dependent loads; in pass 1 a wave would wait for it whenever one of
+   * its 64 requests needed one (config 5: most iterations), listed they run
+   * side by side.  Nothing to do -> no pass at all. */
+  wait_vm0();   /* no window load still writes the staging area (reused below) */
   __syncthreads();
 #ifdef RHP_STAMPS
   if (lane == 0) g_stamps[((blockIdx.x * WAVES + (tid >> 6)) % 8192) * kStampSlots + 14] = __builtin_amdgcn_s_memrealtime();
@@ -901,39 +897,85 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #endif
   if (*wg_deferred) {
     typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-    for (uint32_t i = wg_lo + tid; i < wg_hi; i += WAVES * 64) {
-      /* what a request needs first, in one round trip: in http mode the hint
-       * left in its http record says what to do (and holds ret), so neither
-       * the request record is read nor its flags written back */
-      const uint64_t off = p.offsets[i], end = p.offsets[i + 1];
-      uint32_t f = 0, ret = 0;
-      u32x4a4 hint = u32x4a4{0u, 0u, 0u, 0u};
-      if (http) {
-        hint = *GLOBAL(const u32x4a4, &p.http[i]);
-        f = hint[1] & (kHintExact | kHintFrame);
-        ret = hint[1] & 0xffffu;
-      } else {
-        f = (p.reqs[i].flags & kDeferExact) ? kHintExact : 0u;
+    /* what a request needs first: in http mode the hint left in its http
+     * record says what to do (and holds ret), so neither the request record is
+     * read nor its flags written back.  Pass 1 fetches it one request ahead. */
+    struct Head {
+      uint64_t off, end;
+      u32x4a4 hint;
+      uint32_t f;
+    };
+    auto head = [&](uint32_t k) {
+      Head h = {0, 0, u32x4a4{0u, 0u, 0u, 0u}, 0u};
+      if (k < wg_hi) {
+        h.off = p.offsets[k];
+        h.end = p.offsets[k + 1];
+        if (http) h.hint = *GLOBAL(const u32x4a4, &p.http[k]);
+        else h.f = p.reqs[k].flags;
       }
+      return h;
+    };
+    auto what = [&](const Head &h) {
+      return http ? h.hint[1] & (kHintExact | kHintFrame) : (h.f & kDeferExact) ? kHintExact : 0u;
+    };
+    /* the serial paths; http_frame_fast declined (or the request is exact):
+     * its http record still holds the hint */
+    auto finish_slow = [&](uint32_t i, const Head &h) {
+      const uint32_t f = what(h);
+      if (f & kHintExact) {
+        finish_exact(p, i, h.off, h.end - h.off);
+      } else {
+        const uint32_t cand = h.hint[0];
+        http_frame(p.bytes_rw + h.off, h.end - h.off, p.reqs[i], p.hdrs + (uint64_t) i * p.hs_req, p.hs_hdr,
+                   &p.http[i], (cand >> 31) ? ~0ull : (uint64_t) (cand & 0x3fffffffu));
+      }
+    };
+    uint32_t *slow = reinterpret_cast<uint32_t *>(lds + kLdsTable);   /* the staging area, idle now */
+    uint32_t *slow_n = wg_counter + 4;                                 /* 0 since the prologue */
+    constexpr uint32_t kSlowCap = WAVES * kStageWave / 4;
+#ifdef RHP_STAMPS
+    unsigned long long c0 = 0, c1 = 0;
+    RHP_STAMP(c0);
+#endif
+    Head nx = head(wg_lo + tid);
+    for (uint32_t i = wg_lo + tid; i < wg_hi; i += WAVES * 64) {
+      const Head cur = nx;
+      nx = head(i + WAVES * 64);
+      const uint32_t f = what(cur);
       if (!f) continue;
+      bool later = (f & kHintExact) != 0;
+      if (!later)
+        later = !http_frame_fast(p.bytes_rw + cur.off, cur.end - cur.off, (int32_t) (cur.hint[1] & 0xffffu),
+                                 &p.http[i], cur.hint[0], cur.hint[2], cur.hint[3]);
 #ifdef RHP_STAMPS
-      unsigned long long c0 = 0, c1 = 0;
-      RHP_STAMP(c0);
+      rp[3] += __popcll(__builtin_amdgcn_ballot_w64(!later));
 #endif
-      if (f & kHintExact) finish_exact(p, i, off, end - off);
+      if (later) {
+        const uint32_t at = atomicAdd(slow_n, 1u);
+        if (at < kSlowCap) slow[at] = i;
+        else finish_slow(i, cur);   /* list full (a range of > kSlowCap such requests) */
+      }
+    }
 #ifdef RHP_STAMPS
-      RHP_STAMP(c1);
-      rp[0] += c1 - c0;
-      rp[2] += __popcll(__builtin_amdgcn_ballot_w64((f & kHintExact) != 0));
-      c0 = c1;
+    RHP_STAMP(c1);
+    rp[1] += c1 - c0;
 #endif
-      if (f & kHintFrame) finish_http(p, i, off, end - off, (int32_t) ret, hint[0], hint[2], hint[3]);
+    __syncthreads();
 #ifdef RHP_STAMPS
-      RHP_STAMP(c1);
-      rp[1] += c1 - c0;
-      rp[3] += __popcll(__builtin_amdgcn_ballot_w64((f & kHintFrame) != 0));
+    RHP_STAMP(c0);
+#endif
+    const uint32_t ns = min(*slow_n, kSlowCap);
+    for (uint32_t k = tid; k < ns; k += WAVES * 64) {
+      const uint32_t i = slow[k];
+      finish_slow(i, head(i));
+#ifdef RHP_STAMPS
+      rp[2] += __popcll(__builtin_amdgcn_ballot_w64(true));
 #endif
     }
+#ifdef RHP_STAMPS
+    RHP_STAMP(c1);
+    rp[0] += c1 - c0;
+#endif
   }
 #ifdef RHP_STAMPS
   if (lane == 0) {

@@ -62,6 +62,6 @@ for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, 1), (r
     print(f"   idle lane-iterations: {ni_.sum():.0f}, of them while the pool had requests {il.sum():.0f}; "
           f"iterations after the pool ran dry: {dry.mean():.1f} per wave (of {st[used, 5].mean():.1f})")
     rx = st[used, 15:19]
-    print(f"   replay per wave: exact path {rx[:, 0].mean():.0f} cycles ({rx[:, 2].mean():.1f} requests), "
-          f"framing {rx[:, 1].mean():.0f} cycles ({rx[:, 3].mean():.1f} requests)")
+    print(f"   replay per wave: pass 1 (hint framing) {rx[:, 1].mean():.0f} cycles ({rx[:, 3].mean():.1f} requests framed), "
+          f"pass 2 (listed scalar paths) {rx[:, 0].mean():.0f} cycles ({rx[:, 2].mean():.1f} requests)")
     print(f"   workgroups: last wave's loop end {q(ends)}; first wave's {q(firsts)}", flush=True)

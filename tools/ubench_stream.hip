@@ -104,6 +104,26 @@ __global__ void win64(const uint8_t *buf, uint64_t bytes, uint32_t *out)
   clk_end(t, r);
 }
 
+// config 5's access: lane l owns request r (STRIDE bytes apart) and reads its
+// first BYTES (whole 16-B pieces) once; reported GB/s counts the bytes read
+template <int BYTES, int STRIDE>
+__global__ void sparse(const uint8_t *buf, uint64_t bytes, uint32_t *out)
+{
+  unsigned long long t, r;
+  clk_begin(t, r);
+  const uint64_t lanes = (uint64_t) gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  for (uint64_t req = blockIdx.x * blockDim.x + threadIdx.x; req * STRIDE < bytes; req += lanes) {
+    u32x4 v[BYTES / 16];
+#pragma unroll
+    for (int q = 0; q < BYTES / 16; q++) v[q] = *(gq *) (uintptr_t) (buf + req * STRIDE + 16 * q);
+#pragma unroll
+    for (int q = 0; q < BYTES / 16; q++) acc ^= v[q][0] ^ v[q][1] ^ v[q][2] ^ v[q][3];
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+  clk_end(t, r);
+}
+
 // LDS-DMA: per wave, a staging slot of 64 windows x 128 B; instruction i fetches
 // 8 whole lines (windows 8i..8i+7); SLOTS slots in flight, consumed in order
 template <int NT, int SLOTS, int OFF = 0>
@@ -193,7 +213,8 @@ void run_w(const char *name, F fn, uint8_t *dst, uint64_t lines, uint32_t *out)
 }
 
 template <class F>
-void run(const char *name, F fn, int grid, int block, size_t lds, const uint8_t *buf, uint64_t bytes, uint32_t *out)
+void run(const char *name, F fn, int grid, int block, size_t lds, const uint8_t *buf, uint64_t bytes, uint32_t *out,
+         double useful = 1.0)
 {
   if (lds) CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
   hipEvent_t a, b;
@@ -217,7 +238,7 @@ void run(const char *name, F fn, int grid, int block, size_t lds, const uint8_t 
       mhz = c[1] ? (double) c[0] / (double) c[1] * 100.0 : 0;
     }
   }
-  printf("%-34s grid %5d x %4d  %8.1f GB/s  %.3f ms  clock %.0f MHz\n", name, grid, block, bytes / (best * 1e-3) / 1e9, best, mhz);
+  printf("%-34s grid %5d x %4d  %8.1f GB/s  %.3f ms  clock %.0f MHz\n", name, grid, block, bytes * useful / (best * 1e-3) / 1e9, best, mhz);
   fflush(stdout);
 }
 
@@ -240,6 +261,18 @@ int main(int argc, char **argv)
     run_w("write 64 B of 128 (4 x 16 B)", wrec<64, 16>, dst, lines, out);
     run_w("write 128 B of 128 (8 x 16 B)", wrec<128, 16>, dst, lines, out);
     run_w("write 16 B of 128 (1 x 16 B)", wrec<16, 16>, dst, lines, out);
+    return 0;
+  }
+  if (only[0] == 's') {   /* sparse reads: header bytes of 1 KiB requests; GB/s of bytes read */
+    for (int wpc : {16, 32}) {
+      const int block = 256, grid = cus * wpc / 4;
+      char name[64];
+      snprintf(name, sizeof name, "sparse 128/1024 waves/CU %d", wpc); run(name, sparse<128, 1024>, grid, block, 0, buf, bytes, out, 1.0 / 8);
+      snprintf(name, sizeof name, "sparse 192/1024 waves/CU %d", wpc); run(name, sparse<192, 1024>, grid, block, 0, buf, bytes, out, 3.0 / 16);
+      snprintf(name, sizeof name, "sparse 256/1024 waves/CU %d", wpc); run(name, sparse<256, 1024>, grid, block, 0, buf, bytes, out, 1.0 / 4);
+      snprintf(name, sizeof name, "sparse 384/1024 waves/CU %d", wpc); run(name, sparse<384, 1024>, grid, block, 0, buf, bytes, out, 3.0 / 8);
+      snprintf(name, sizeof name, "dense 256/256 waves/CU %d", wpc); run(name, sparse<256, 256>, grid, block, 0, buf, bytes, out);
+    }
     return 0;
   }
   if (only[0]) {

@@ -80,10 +80,12 @@ enum : uint32_t {
   kHintFrame = 0x80000000u,
   /* workgroup pool area after the staging buffers: counters, then the long-
    * request bitmap (ranges up to kOrderSpan requests) and list */
-  kPoolWords = 8,                                /* counter, replay flag, list length, list cursor */
+  kPoolWords = 8,                                /* counter, replay flag, long-list length, long-list
+                                                    cursor, slow-list length, defer-list length */
   kOrderSpan = 8192,
   kListCap = 1536,
-  kPoolBytes = 4 * kPoolWords + kOrderSpan / 8 + 2 * kListCap
+  kDeferCap = 480,                               /* the replay's list (defer) */
+  kPoolBytes = 4 * kPoolWords + kOrderSpan / 8 + 2 * kListCap + 2 * kDeferCap
 };
 static_assert(idx2(S_DONE, 0) == kPark, "parked lanes sit in DONE");
 
@@ -251,6 +253,43 @@ __device__ __forceinline__ bool http_frame_fast(const uint8_t *b, uint64_t len, 
   return true;
 }
 
+/* http_frame_fast in the DFA loop (the late-issue kernel's finalize): the
+ * same decisions from one 28-byte load at the candidate's name -- a fast-path
+ * record has exactly one SP after the colon, so a Content-Length value starts
+ * 16 bytes after its name; values over 12 bytes decline (the replay frames
+ * them).  Returns false when the replay must frame the request. */
+__device__ __forceinline__ bool http_frame_loop(const uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x,
+                                                uint32_t cand, uint32_t crec_lo, uint32_t crec_hi)
+{
+  const int64_t n = ret;
+  rhp_http_t o = {1, 0, (uint64_t) n, 0};
+  const uint32_t hdr = cand & 0x3fffffffu;
+  if (!(cand & 0x40000000u) && hdr != 0) {   /* not GET (http.c:198-202), some candidate */
+    if ((cand >> 31) || (hdr & (hdr - 1)) != 0) return false;
+    const uint32_t name_off = crec_lo & 0xffffu, name_len = crec_lo >> 16;
+    const uint32_t value_len = crec_hi >> 16;
+    if (name_len != 14u) return false;   /* 17: Transfer-Encoding or neither -- the replay */
+    uint32_t d[7];
+    load28(b + name_off, d);
+    if (name_is(d, "content-length") && value_len != 0) {
+      if (value_len > 12u) return false;
+      uint32_t st = 0;
+      bool neg = false, ovf = false;
+      uint64_t v = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < 12; j++) num_step(j < value_len ? RHP_BYTE(d, j + 16) : 0u, st, neg, ovf, v);
+      const uint64_t size = ovf ? ~0ull : neg ? 0 - v : v;
+      if (len < (uint64_t) n + size) {
+        o.result = 0; o.consumed = 0;
+      } else {
+        o.body_kind = 1; o.body_len = size; o.consumed = (uint64_t) n + size;
+      }
+    }
+  }
+  *x = o;
+  return true;
+}
+
 /* Params pointers are generic in the kernel's view (they sit in a struct);
  * the hot stores go through explicit global-address-space pointers so they are
  * global_store (VM counter only), not flat_store (VM + LGKM). */
@@ -300,6 +339,16 @@ __device__ __forceinline__ void store_req(rhp_req_t *dst, const rhp_req_t &r)
   __builtin_memcpy(&v, &r, sizeof r);
   *GLOBAL(u32x4, dst) = v;
 }
+__device__ __forceinline__ void store_http(rhp_http_t *dst, const rhp_http_t &x)
+{
+  typedef uint32_t u32x2a8 __attribute__((ext_vector_type(2), aligned(8)));
+  u32x2a8 v[3];
+  __builtin_memcpy(v, &x, sizeof x);
+  __attribute__((address_space(1))) u32x2a8 *q = GLOBAL(u32x2a8, dst);
+  q[0] = v[0];
+  q[1] = v[1];
+  q[2] = v[2];
+}
 __device__ __forceinline__ void store_http_bad(rhp_http_t *dst)
 {
   /* {result -1, body_kind 0, consumed 0, body_len 0} */
@@ -321,7 +370,7 @@ __device__ __forceinline__ void store_http_bad(rhp_http_t *dst)
  * events of the window walked in the previous iteration) -- the same request
  * unless the lane switched between the two windows.
  */
-template <int WAVES>
+template <int WAVES, bool LATE>
 __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel(Params p)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -386,6 +435,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   int32_t wpos = 0;                    /* request-relative position of the window's first byte */
   bool wact = false;                   /* wcur is live: its walk has not ended */
   uint32_t wcur = 0, wlen = 0, wget = 0, cur_ptr = 0;
+  uint32_t woff = 0;                   /* wcur's first byte, offset from base (LATE http framing) */
   uint32_t ev[kEvWords];               /* events of the window being walked (32 bytes per word) */
   bool pend_ok = false;                /* pend: the lane's next request */
   uint32_t pend = 0;
@@ -406,7 +456,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * name length is 14 or 17 (bit 31: such a header at index >= 30), bit 30 =
    * the method is GET; crec = the first such header's record */
   bool dhas = false;
-  uint32_t dcur = 0, dlen = 0, st_prev = kPark;
+  uint32_t dcur = 0, dlen = 0, st_prev = kPark, doff = 0;
   int32_t dpos = 0;                    /* position of the decoded window's first byte */
   uint32_t evp[kEvWords];              /* its events */
   uint32_t kn = 0, me = 0, pe = 0, rl = 0, nh = 0, ls = 0, t = 0, pco = 0, ovf = 0;
@@ -453,17 +503,12 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     }
   };
 
-  /* the long-request scan (see order_on), once, over the part of the range the
-   * first refill did not hand out */
+  /* the long-request scan (see order_on): every request of the range longer
+   * than twice its mean goes into the long list (and bitmap) */
+  const uint32_t span_n = wg_hi - wg_lo;
   auto scan_long = [&]() {
-    const uint32_t span_n = wg_hi - wg_lo;
-    if (span_n <= first_n) return;
-    /* long: length * count > 2 * the range's bytes (no division) */
     const uint64_t twice = 2u * (o_hi - o_lo);
-    /* a wave scans its slice only if its own first requests (offsets already
-     * loaded) include a long one: uniform batches skip the scan */
-    if (!__ballot(pend_ok && (uint64_t) (pend_o1 - pend_o0) * span_n > twice)) return;
-    for (uint32_t k = first_n + tid; k < span_n; k += WAVES * 64) {
+    for (uint32_t k = tid; k < span_n; k += WAVES * 64) {
       const uint64_t o0 = p.offsets[wg_lo + k], o1 = p.offsets[wg_lo + k + 1];
       if ((o1 - o0) * span_n > twice) {
         const uint32_t at = atomicAdd(list_n, 1u);
@@ -473,6 +518,17 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         }
       }
     }
+  };
+
+  /* the replay's work list: requests finalize deferred, as offsets in the
+   * range (u16); on overflow (or ranges over 64K requests) the replay scans
+   * the whole range */
+  uint32_t *defer_n = wg_counter + 5;
+  uint16_t *defer_list = long_list + kListCap;
+  auto defer = [&](uint32_t i) {
+    *wg_deferred = 1u;
+    const uint32_t at = atomicAdd(defer_n, 1u);
+    if (at < kDeferCap) defer_list[at] = (uint16_t) (i - wg_lo);
   };
 
   /* ---- decode ----
@@ -633,17 +689,30 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     u32x4 rq = u32x4{0u, 0u, 0xff000000u, 0u};   /* minor_version -1 */
     if (ok) {
       rq = u32x4{term_pos + 1u, (rl & 0xffffu) | ((rl + 1u) << 16), (rl >> 16) | (((kn >> 3) & 1u) << 24), nh};
-      if (http) {   /* framing: replay, from the hints left in the record it will overwrite */
-        *wg_deferred = 1u;
-        typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-        *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{cand, kHintFrame | (term_pos + 1u), crec_lo, crec_hi};
+      if (http) {
+        /* framing (http.c:196-218): in the late-issue kernel the common cases
+         * (GET, no Content-Length / Transfer-Encoding candidate, one
+         * Content-Length) are framed here, the candidate's line read back from
+         * L2 right after its walk; the rest in the replay, from the hints left
+         * in the record it will overwrite */
+        bool framed = false;
+        if constexpr (LATE) {
+          rhp_http_t x;
+          framed = http_frame_loop(wbytes + doff, dlen, (int32_t) (term_pos + 1u), &x, cand, crec_lo, crec_hi);
+          if (framed) store_http(p.http + dcur, x);
+        }
+        if (!framed) {
+          defer(dcur);
+          typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+          *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{cand, kHintFrame | (term_pos + 1u), crec_lo, crec_hi};
+        }
       }
     } else if (bad) {
       rq[0] = 0xffffffffu;   /* -1 */
       if (http) store_http_bad(p.http + dcur);
     } else {
       rq[3] = (uint32_t) kDeferExact << 16;   /* exact path: replay */
-      *wg_deferred = 1u;
+      defer(dcur);
       if (http) {
         typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
         *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{0u, kHintExact, 0u, 0u};
@@ -716,7 +785,13 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
      * straddle lines share their edge lines with the neighbouring requests'
      * windows, which then hit in L2 (non-temporal: config 3 -5 %) */
     const bool aligned = !(nw & 3u) || ((uint32_t) (uintptr_t) (wbytes + src) & (kBlock - 1u)) == 0;
-    const bool nt = !__builtin_amdgcn_ballot_w64(!aligned);
+#ifndef RHP_LATE_NT
+#define RHP_LATE_NT 0
+#endif
+    /* the late-issue (http) kernel frames requests from their header lines
+     * right after the walk: those lines must still be in L2, so its windows
+     * are never non-temporal */
+    const bool nt = (!LATE || RHP_LATE_NT) && !__builtin_amdgcn_ballot_w64(!aligned);
     /* one branch per issue, not one per load (the cache policy is an immediate) */
 #define RHP_ISSUE_LOADS(AUX)                                                                             \
     _Pragma("unroll") for (int i = 0; i < (int) kParts; i++) {                                           \
@@ -729,6 +804,16 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #undef RHP_ISSUE_LOADS
   };
 
+  /* Uneven ranges (config 3) order the hand-out from the first request on;
+   * the test reads the first 64 requests of the range, the same in every wave,
+   * so every wave takes the same branch without a barrier */
+  const bool may_order = order_on && span_n > first_n;
+  uint32_t s0 = 0, s1 = 0;
+  if (may_order) {
+    const uint32_t *so = reinterpret_cast<const uint32_t *>(p.offsets + wg_lo + min(lane, span_n - 1u));
+    s0 = *GLOBAL(const uint32_t, so);
+    s1 = *GLOBAL(const uint32_t, so + 2);
+  }
   if (tid < first_n) take(wg_lo + tid);
   /* the table into LDS, the pool counter past the requests handed out, the
    * long-request bitmap cleared */
@@ -739,16 +824,33 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   }
   for (uint32_t k = tid; k < kPoolWords + kOrderSpan / 32; k += WAVES * 64)
     reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave)[k] = k == 0 ? first_n : 0u;
-  /* The first windows: issue them, then (while they land) the long-request
-   * scan; the barriers make the pool area initialized before the scan and the
-   * list complete before any wave's next refill. */
   wait_vm0();   /* the pending offsets */
-  nw = pend_ok ? ((pend_o0 & ~3u) - (uint32_t) base) | 2u : 0u;
-  issue();
-  __syncthreads();
-  if (order_on) scan_long();
-  __syncthreads();
-  first_iter = false;
+  const bool uneven =
+      may_order && __builtin_amdgcn_ballot_w64((uint64_t) (s1 - s0) * span_n > 2u * (o_hi - o_lo)) != 0;
+  if (uneven) {
+    /* every request longer than twice the range's mean is handed out before
+     * the others, the first hand-out included: a long request never waits
+     * behind another one in a lane (the barriers: the pool area initialized
+     * before the scan; the list complete and the counter reset before the
+     * first refill) */
+    pend_ok = false;
+    __syncthreads();
+    if (tid == 0) *wg_counter = 0;
+    scan_long();
+    __syncthreads();
+    first_iter = false;
+    refill_pend();
+    wait_vm0();
+    nw = pend_ok ? ((pend_o0 & ~3u) - (uint32_t) base) | 2u : 0u;
+    issue();
+  } else {
+    /* the first windows, then the barrier that makes the pool area
+     * initialized before any wave's first refill */
+    nw = pend_ok ? ((pend_o0 & ~3u) - (uint32_t) base) | 2u : 0u;
+    issue();
+    __syncthreads();
+    first_iter = false;
+  }
 
   /*
    * One iteration = one 128-byte window per lane.
@@ -779,6 +881,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     if (nw_kind == 2) {   /* pend's first window: the walk switches to pend */
       wcur = pend;
       wlen = p_o1 - p_o0;
+      if constexpr (LATE) woff = p_o0 - (uint32_t) base;
       pend_ok = false;
       const uint32_t mis = p_o0 & 3u;
       st = idx2(mis == 0 ? S_METHOD0 : mis == 1 ? S_SKIP1 : mis == 2 ? S_SKIP2 : S_SKIP3, 0);
@@ -795,42 +898,86 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const bool pend_ready = pend_ok;   /* assigned before this block: its offsets are valid */
     /* [D] */
     refill_pend();
-    /* [E] next window: continuation of wcur, else the first window of a ready pend */
-    nw = 0;
-    if (walking && (uint32_t) (wpos + (int32_t) kBlock) < wlen) nw = (cur_ptr + kBlock) | 1u;
-    else if (pend_ready) nw = ((p_o0 & ~3u) - (uint32_t) base) | 2u;
-    wait_lgkm0();   /* [A]'s reads of the buffer are done */
-    issue();
-#ifdef RHP_STAMPS
-    wait_lgkm0();
-    RHP_STAMP(t1); acc[1] += t1 - t0; t0 = t1;
-#endif
-    /* [F] walk + decode of the previous window */
-    decode_begin();
-    if (__builtin_amdgcn_ballot_w64(dhas)) decode_window();
-#pragma unroll
-    for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
-#ifdef RHP_STAMPS
-    wait_vm0(); wait_lgkm0();
-    RHP_STAMP(t1); acc[2] += t1 - t0; t0 = t1;
-#endif
     const bool any_walk = __builtin_amdgcn_ballot_w64(walking) != 0;
+    const bool any_dec = __builtin_amdgcn_ballot_w64(dhas) != 0;
 #ifdef RHP_STAMPS
     n_walk += __popcll(__builtin_amdgcn_ballot_w64(walking));
     n_idle += __popcll(__builtin_amdgcn_ballot_w64(!walking));
     if (!pool_dry) n_idle_live += __popcll(__builtin_amdgcn_ballot_w64(!walking));
     else n_dry++;
 #endif
-    const bool any_dec = __builtin_amdgcn_ballot_w64(dhas) != 0;
-    if (any_walk) {
-      if (!walking) st = kPark;   /* idle lanes step in the parked terminal state */
-      walk();
+    if constexpr (!LATE) {
+      /* [E] next window: continuation of wcur, else the first window of a ready pend */
+      nw = 0;
+      if (walking && (uint32_t) (wpos + (int32_t) kBlock) < wlen) nw = (cur_ptr + kBlock) | 1u;
+      else if (pend_ready) nw = ((p_o0 & ~3u) - (uint32_t) base) | 2u;
+      wait_lgkm0();   /* [A]'s reads of the buffer are done */
+      issue();
+#ifdef RHP_STAMPS
+      wait_lgkm0();
+      RHP_STAMP(t1); acc[1] += t1 - t0; t0 = t1;
+#endif
+      /* [F] walk + decode of the previous window */
+      decode_begin();
+      if (any_dec) decode_window();
+#pragma unroll
+      for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
+#ifdef RHP_STAMPS
+      wait_vm0(); wait_lgkm0();
+      RHP_STAMP(t1); acc[2] += t1 - t0; t0 = t1;
+#endif
+      if (any_walk) {
+        if (!walking) st = kPark;   /* idle lanes step in the parked terminal state */
+        walk();
+      }
+    } else {
+      /* [F] walk, then decode the walked window at once (not one behind): a
+       * request is finalized -- and framed, from its header lines while they
+       * are still in L2 -- in the iteration that walks its last window; [E]
+       * then knows whether wcur's walk ended (no continuation is fetched past
+       * a terminal: a body is never loaded), and a request taken in [D] is
+       * ready (its offsets landed meanwhile), so a lane never idles an
+       * iteration between two requests */
+      (void) any_dec;
+#pragma unroll
+      for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
+      if (any_walk) {
+        if (!walking) st = kPark;
+        walk();
+      }
+      if (walking && wnew) {
+        dcur = wcur;
+        dlen = wlen;
+        doff = woff;
+        kn = me = pe = rl = nh = ls = t = pco = ovf = 0;
+        cand = wget;
+        crec_lo = crec_hi = 0;
+      }
+      dhas = walking;
+      dpos = wpos;
+      st_prev = st;
+#pragma unroll
+      for (int w = 0; w < (int) kEvWords; w++) evp[w] = ev[w];
+      decode_begin();
+      if (any_walk) decode_window();
+      const bool done = any_walk ? decode_end() : false;
+      /* the walk of wcur ends with this window: finalized (a terminal, a
+       * max_headers stop), or its last byte */
+      if (walking && (done || is_done2(st) || is_err2(st) || is_slow2(st) ||
+                      (uint32_t) (wpos + (int32_t) kBlock) >= wlen))
+        wact = false;
+      nw = 0;
+      if (walking && wact) nw = (cur_ptr + kBlock) | 1u;
+      else if (pend_ok) nw = ((pend_o0 & ~3u) - (uint32_t) base) | 2u;
+      wait_lgkm0();
+      issue();
     }
 #ifdef RHP_STAMPS
     wait_lgkm0();
     RHP_STAMP(t1); acc[3] += t1 - t0; t0 = t1;
 #endif
     /* [G] */
+    if constexpr (!LATE) {
     const bool done = any_dec ? decode_end() : false;
     if (done && !wnew) wact = false;   /* decoded request ended (max_headers stop): stop its walk */
     /* hand the decode over to the walked window */
@@ -838,6 +985,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (wnew) {
         dcur = wcur;
         dlen = wlen;
+        if constexpr (LATE) doff = woff;
         kn = me = pe = rl = nh = ls = t = pco = ovf = 0;
         cand = wget;
         crec_lo = crec_hi = 0;
@@ -851,6 +999,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (is_done2(st) || is_err2(st) || is_slow2(st) || (uint32_t) (wpos + (int32_t) kBlock) >= wlen) wact = false;
     } else {
       dhas = false;
+    }
     }
     wpos += (int32_t) kBlock;
 #ifdef RHP_STAMPS
@@ -937,10 +1086,18 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     unsigned long long c0 = 0, c1 = 0;
     RHP_STAMP(c0);
 #endif
-    Head nx = head(wg_lo + tid);
-    for (uint32_t i = wg_lo + tid; i < wg_hi; i += WAVES * 64) {
+    /* the deferred requests: the list finalize kept, or the whole range when
+     * it overflowed */
+    const uint32_t nd = *defer_n;
+    const bool use_list = nd <= kDeferCap && wg_hi - wg_lo <= 65536u;
+    const uint32_t cnt = use_list ? nd : wg_hi - wg_lo;
+    auto req_at = [&](uint32_t k) { return wg_lo + (use_list ? (uint32_t) defer_list[k] : k); };
+    auto head_at = [&](uint32_t k) { return head(k < cnt ? req_at(k) : wg_hi); };
+    Head nx = head_at(tid);
+    for (uint32_t k = tid; k < cnt; k += WAVES * 64) {
+      const uint32_t i = req_at(k);
       const Head cur = nx;
-      nx = head(i + WAVES * 64);
+      nx = head_at(k + WAVES * 64);
       const uint32_t f = what(cur);
       if (!f) continue;
       bool later = (f & kHintExact) != 0;
@@ -1003,7 +1160,7 @@ namespace {
  * the implementation choice (rhp_set_impl, diagnostics) is per thread. */
 constexpr int kMaxDevices = 64;
 std::atomic<int> g_cus[kMaxDevices];
-std::atomic<uint32_t> g_attr[kMaxDevices];   /* bit w/4: the LDS attribute of rhp_dfa_kernel<w> is set */
+std::atomic<uint32_t> g_attr[kMaxDevices];   /* bit 2(w/4)+late: the LDS attribute of rhp_dfa_kernel<w, late> is set */
 thread_local int t_impl = RHP_IMPL_DFA;
 
 int device_cus(int dev, int *cus)
@@ -1018,14 +1175,14 @@ int device_cus(int dev, int *cus)
   return 0;
 }
 
-template <int WAVES>
+template <int WAVES, bool LATE>
 int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
 {
   const size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes;
-  const uint32_t bit = 1u << (WAVES / 4);
+  const uint32_t bit = 1u << (2 * (WAVES / 4) + (LATE ? 1 : 0));
   if (!(g_attr[dev].load(std::memory_order_acquire) & bit)) {
     /* idempotent: two threads of one device may both set it */
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES, LATE>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds_bytes);
     if (e != hipSuccess) return (int) e;
     g_attr[dev].fetch_or(bit, std::memory_order_release);
@@ -1037,7 +1194,7 @@ int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
   /* each workgroup owns a contiguous n/grid share of the requests */
   Params q = prm;
   q.span = (prm.n + grid - 1) / grid;
-  hipLaunchKernelGGL(rhp_dfa_kernel<WAVES>, dim3(grid), dim3(WAVES * 64), lds_bytes, s, q);
+  hipLaunchKernelGGL((rhp_dfa_kernel<WAVES, LATE>), dim3(grid), dim3(WAVES * 64), lds_bytes, s, q);
   return (int) hipGetLastError();
 }
 
@@ -1048,6 +1205,19 @@ int dfa_waves()   /* RHP_WAVES (experiments): waves per workgroup */
     return e ? atoi(e) : 16;
   }();
   return w;
+}
+/* RHP_LATE (A/B): 0 the early window issue everywhere, 1 late issue in http
+ * mode, 2 late issue in both modes */
+#ifndef RHP_LATE_DEFAULT
+#define RHP_LATE_DEFAULT 1
+#endif
+bool late_issue(uint32_t mode)
+{
+  static const int l = [] {
+    const char *e = getenv("RHP_LATE");
+    return e ? atoi(e) : RHP_LATE_DEFAULT;
+  }();
+  return l >= 2 || (l == 1 && mode == RHP_MODE_HTTP);
 }
 }  // namespace
 
@@ -1124,10 +1294,12 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
     hipLaunchKernelGGL(rhp_exact_kernel, dim3(grid), dim3(256), 0, s, prm);
     return (int) hipGetLastError();
   }
+  const bool late = late_issue(b->mode);
+  if (late) return launch_dfa<16, true>(prm, s, dev, cus);
   switch (dfa_waves()) {
-  case 8: return launch_dfa<8>(prm, s, dev, cus);
-  case 12: return launch_dfa<12>(prm, s, dev, cus);
-  default: return launch_dfa<16>(prm, s, dev, cus);
+  case 8: return launch_dfa<8, false>(prm, s, dev, cus);
+  case 12: return launch_dfa<12, false>(prm, s, dev, cus);
+  default: return launch_dfa<16, false>(prm, s, dev, cus);
   }
 }
 

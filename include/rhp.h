@@ -124,7 +124,9 @@ int rhp_parse_batch(const rhp_batch_t *batch, void *stream);
 /* Which kernel implementation rhp_parse_batch uses (diagnostics / A-B tests). */
 enum rhp_impl {
   RHP_IMPL_DFA = 0,    /* lane-per-request byte DFA with LDS tables (default) */
-  RHP_IMPL_EXACT = 1   /* lane-per-request exact scalar path only (slow reference path) */
+  RHP_IMPL_EXACT = 1,  /* lane-per-request exact scalar path only (slow reference path) */
+  RHP_IMPL_DFA_LATE = 2 /* the DFA kernel in its late-issue form in both modes (the default
+                           uses that form in RHP_MODE_HTTP only) */
 };
 int rhp_set_impl(int impl);   /* per calling thread */
 

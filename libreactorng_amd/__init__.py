@@ -28,7 +28,7 @@ RHP_RET_TOOLONG = -3
 RHP_WORK_WORDS = 64
 MODE_PHR, MODE_HTTP = 0, 1
 LAYOUT_REQUEST_MAJOR, LAYOUT_HEADER_MAJOR = 0, 1
-IMPL_DFA, IMPL_EXACT = 0, 1
+IMPL_DFA, IMPL_EXACT, IMPL_DFA_LATE = 0, 1, 2
 RHP_NAME_NULL = 0xFFFF
 F_EXACT = 0x1
 

@@ -78,6 +78,18 @@ enum : uint32_t {
    * finalize leaves in http[i] (ret in the low 16 bits) */
   kHintExact = 0x40000000u,
   kHintFrame = 0x80000000u,
+  /* fr: the first framing candidate's evaluation (late-issue kernel) */
+  kFrCarry = 1u,      /* its name is Content-Length, its value is being read (digits in fv) */
+  kFrTeName = 2u,     /* its name is Transfer-Encoding, its record not complete yet */
+  kFrCl = 4u,         /* a Content-Length with a value: fv = strtoull(value) */
+  kFrTe = 8u,         /* a Transfer-Encoding with a value */
+  kFrDefer = 16u,     /* not evaluated here: the replay frames the request */
+  kFrDigits = 32u,    /* the number has started (a sign or a digit was read) */
+  kFrNeg = 64u,       /* ... with a '-' */
+  kFrStop = 128u,     /* ... and ended (a non-digit was read) */
+  kFrCountSh = 8u,    /* bits 8..15: value bytes read */
+  kFrMaxValue = 19u,  /* longer values are left to the replay (19 digits cannot overflow) */
+  kFrNeither = 1u << 16,   /* its name, read while its line was open, is neither */
   /* workgroup pool area after the staging buffers: counters, then the long-
    * request bitmap (ranges up to kOrderSpan requests) and list */
   kPoolWords = 8,                                /* counter, replay flag, long-list length, long-list
@@ -116,8 +128,8 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
  * still had requests, 13 iterations after the pool ran dry, 14 the replay's
  * start (after the workgroup barrier), 15 / 16 the wave's shader cycles in the
  * replay's pass 2 (listed scalar paths) / pass 1, 17 requests it ran in pass 2,
- * 18 requests it framed in pass 1 */
-enum : uint32_t { kStampSlots = 20 };
+ * 18 requests it framed in pass 1, 19 the prologue's loads landed */
+enum : uint32_t { kStampSlots = 24 };
 __device__ unsigned long long g_stamps[8192 * kStampSlots];
 #define RHP_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); (t) = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0); } while (0)
@@ -253,42 +265,9 @@ __device__ __forceinline__ bool http_frame_fast(const uint8_t *b, uint64_t len, 
   return true;
 }
 
-/* http_frame_fast in the DFA loop (the late-issue kernel's finalize): the
- * same decisions from one 28-byte load at the candidate's name -- a fast-path
- * record has exactly one SP after the colon, so a Content-Length value starts
- * 16 bytes after its name; values over 12 bytes decline (the replay frames
- * them).  Returns false when the replay must frame the request. */
-__device__ __forceinline__ bool http_frame_loop(const uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x,
-                                                uint32_t cand, uint32_t crec_lo, uint32_t crec_hi)
-{
-  const int64_t n = ret;
-  rhp_http_t o = {1, 0, (uint64_t) n, 0};
-  const uint32_t hdr = cand & 0x3fffffffu;
-  if (!(cand & 0x40000000u) && hdr != 0) {   /* not GET (http.c:198-202), some candidate */
-    if ((cand >> 31) || (hdr & (hdr - 1)) != 0) return false;
-    const uint32_t name_off = crec_lo & 0xffffu, name_len = crec_lo >> 16;
-    const uint32_t value_len = crec_hi >> 16;
-    if (name_len != 14u) return false;   /* 17: Transfer-Encoding or neither -- the replay */
-    uint32_t d[7];
-    load28(b + name_off, d);
-    if (name_is(d, "content-length") && value_len != 0) {
-      if (value_len > 12u) return false;
-      uint32_t st = 0;
-      bool neg = false, ovf = false;
-      uint64_t v = 0;
-#pragma unroll
-      for (uint32_t j = 0; j < 12; j++) num_step(j < value_len ? RHP_BYTE(d, j + 16) : 0u, st, neg, ovf, v);
-      const uint64_t size = ovf ? ~0ull : neg ? 0 - v : v;
-      if (len < (uint64_t) n + size) {
-        o.result = 0; o.consumed = 0;
-      } else {
-        o.body_kind = 1; o.body_len = size; o.consumed = (uint64_t) n + size;
-      }
-    }
-  }
-  *x = o;
-  return true;
-}
+/* the framing names as types (compile-time literals for the LDS compare) */
+struct LitCl { static constexpr char s[] = "content-length"; };
+struct LitTe { static constexpr char s[] = "transfer-encoding"; };
 
 /* Params pointers are generic in the kernel's view (they sit in a struct);
  * the hot stores go through explicit global-address-space pointers so they are
@@ -461,6 +440,14 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   uint32_t evp[kEvWords];              /* its events */
   uint32_t kn = 0, me = 0, pe = 0, rl = 0, nh = 0, ls = 0, t = 0, pco = 0, ovf = 0;
   uint32_t cand = 0, crec_lo = 0, crec_hi = 0;
+  /* http framing in the late-issue kernel (http.c:196-218), from the
+   * staging buffer while the decoded window is still in it: the request's
+   * first framing candidate (a header whose name is 14 or 17 bytes long) is
+   * evaluated when its record completes -- or, when its line is still open
+   * at the window's end, its name and the value bytes so far are, the value's
+   * number carried into the next window.  fr flags (kFr*), fv the number. */
+  uint32_t fr = 0;
+  uint64_t fv = 0;
 #pragma unroll
   for (int w = 0; w < (int) kEvWords; w++) ev[w] = evp[w] = 0;
 
@@ -648,6 +635,94 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #pragma unroll
     for (int q = 0; q < (int) kEvWords; q++) word(mq[q], (uint32_t) dpos + 32u * (uint32_t) q);
   };
+  /* byte at request position x of the decoded window (dpos <= x < dpos + 128),
+   * from the staging buffer (late-issue kernel: the decode runs before the
+   * issue that refills it) */
+  auto win_byte = [&](uint32_t x) __attribute__((always_inline)) {
+    const uint32_t b = x - (uint32_t) dpos;
+    return lds_u8(stage + stage_off(lane, b >> 4) + (b & 15u));
+  };
+  /* case-insensitive name check against a lower-case literal (OR 0x20: the
+   * one non-letter, '-', could only collide with CR, which no name holds) */
+  auto win_name_is = [&](uint32_t at, auto lit) __attribute__((always_inline)) {
+    constexpr uint32_t n = sizeof(lit.s) - 1;
+    uint32_t c[n], diff = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < n; j++) c[j] = win_byte(at + j);   /* all reads first */
+#pragma unroll
+    for (uint32_t j = 0; j < n; j++) diff |= (c[j] | 0x20u) ^ (uint32_t) (uint8_t) lit.s[j];
+    return diff == 0;
+  };
+  /* strtoull (rhp_scalar.h num_step) over value bytes [from, to) of the
+   * window: the value of a fast-path record starts with neither OWS nor a
+   * CTL, so only the sign and the digit run matter */
+  auto win_number = [&](uint32_t from, uint32_t to) __attribute__((always_inline)) {
+    for (uint32_t x = from; x < to && !(fr & kFrStop); x += 4) {
+      uint32_t c4[4];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) c4[k] = win_byte(min(x + k, to - 1u));   /* four reads, one wait */
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) {
+        if (x + k >= to || (fr & kFrStop)) break;
+        const uint32_t c = c4[k], d = c - '0';
+        const uint32_t cnt = ((fr >> kFrCountSh) & 0xffu) + 1u;
+        fr = (fr & ~(0xffu << kFrCountSh)) | (min(cnt, 255u) << kFrCountSh);
+        if (!(fr & kFrDigits) && (c == '+' || c == '-')) {
+          fr |= kFrDigits | (c == '-' ? kFrNeg : 0u);
+        } else if (d < 10u) {
+          fr |= kFrDigits;
+          fv = fv * 10u + d;
+        } else {
+          fr |= kFrStop;
+        }
+      }
+    }
+  };
+  /* the framing candidate's evaluation after a window's decode (see fr) */
+  auto frame_window = [&](uint32_t crec_before) __attribute__((always_inline)) {
+    if (fr & kFrDefer) return;
+    const uint32_t wend = (uint32_t) dpos + kBlock;
+    if ((crec_lo | (cand & 0xbfffffffu)) != crec_before && (cand & 0x3fffffffu) != 0 &&
+        ((cand & 0x3fffffffu) & ((cand & 0x3fffffffu) - 1u)) == 0 && !(cand >> 31)) {
+      /* the first candidate's record completed in this window */
+      const uint32_t name_off = crec_lo & 0xffffu, name_len = crec_lo >> 16;
+      const uint32_t value_off = crec_hi & 0xffffu, value_len = crec_hi >> 16;
+      if (fr & kFrCarry) {   /* Content-Length, value started in an earlier window */
+        win_number(max(value_off, (uint32_t) dpos), value_off + value_len);
+        fr = (fr & ~kFrCarry) | (value_len != 0 ? kFrCl : 0u);   /* an empty value is no Content-Length */
+      } else if (fr & kFrTeName) {
+        fr = (fr & ~kFrTeName) | (value_len != 0 ? kFrTe : 0u);
+      } else if (fr & kFrNeither) {
+        /* nothing to frame */
+      } else if (name_off < (uint32_t) dpos) {
+        fr |= kFrDefer;   /* the name began in an earlier window */
+      } else if (name_len == 14u && win_name_is(name_off, LitCl{})) {
+        if (value_len > kFrMaxValue) fr |= kFrDefer;
+        else if (value_len != 0) { win_number(value_off, value_off + value_len); fr |= kFrCl; }
+      } else if (name_len == 17u && win_name_is(name_off, LitTe{})) {
+        fr |= value_len != 0 ? kFrTe : 0u;
+      }
+      if ((fr & kFrCl) && ((fr >> kFrCountSh) & 0xffu) > kFrMaxValue) fr |= kFrDefer;
+    } else if (t && (cand & 0xbfffffffu) == 0) {
+      /* the first candidate's line may be open at the window's end */
+      const uint32_t nlen = pco - ls;
+      if (fr & kFrCarry) {
+        win_number(max(pco + 2u, (uint32_t) dpos), wend);
+        if (((fr >> kFrCountSh) & 0xffu) > kFrMaxValue) fr |= kFrDefer;
+      } else if (!(fr & (kFrTeName | kFrNeither)) && (nlen == 14u || nlen == 17u)) {
+        if (ls < (uint32_t) dpos) {
+          fr |= kFrDefer;
+        } else if (nlen == 14u && win_name_is(ls, LitCl{})) {
+          fr |= kFrCarry;
+          win_number(pco + 2u, wend);
+        } else if (nlen == 17u && win_name_is(ls, LitTe{})) {
+          fr |= kFrTeName;
+        } else {
+          fr |= kFrNeither;
+        }
+      }
+    }
+  };
   /* set up the decode of the window walked last iteration */
   auto decode_begin = [&]() {
     const uint32_t e = st_prev;
@@ -697,9 +772,26 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
          * in the record it will overwrite */
         bool framed = false;
         if constexpr (LATE) {
-          rhp_http_t x;
-          framed = http_frame_loop(wbytes + doff, dlen, (int32_t) (term_pos + 1u), &x, cand, crec_lo, crec_hi);
-          if (framed) store_http(p.http + dcur, x);
+          /* GET or no candidate: no body; one candidate: its evaluation (a
+           * Content-Length value, or neither name); several, a
+           * Transfer-Encoding with a value (chunked) or no evaluation: the
+           * replay */
+          const uint32_t hdr = cand & 0x3fffffffu, ret = term_pos + 1u;
+          const bool get = (cand & 0x40000000u) != 0;
+          const bool one = !(cand >> 31) && hdr != 0 && (hdr & (hdr - 1)) == 0;
+          if (get || (hdr == 0 && !(cand >> 31)) || (one && !(fr & (kFrDefer | kFrTe | kFrCarry | kFrTeName)))) {
+            rhp_http_t x = {1, 0, (uint64_t) ret, 0};
+            if (!get && (fr & kFrCl)) {
+              const uint64_t size = (fr & kFrNeg) ? 0 - fv : fv;
+              if (dlen < (uint64_t) ret + size) {
+                x.result = 0; x.consumed = 0;
+              } else {
+                x.body_kind = 1; x.body_len = size; x.consumed = (uint64_t) ret + size;
+              }
+            }
+            store_http(p.http + dcur, x);
+            framed = true;
+          }
         }
         if (!framed) {
           defer(dcur);
@@ -785,13 +877,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
      * straddle lines share their edge lines with the neighbouring requests'
      * windows, which then hit in L2 (non-temporal: config 3 -5 %) */
     const bool aligned = !(nw & 3u) || ((uint32_t) (uintptr_t) (wbytes + src) & (kBlock - 1u)) == 0;
-#ifndef RHP_LATE_NT
-#define RHP_LATE_NT 0
-#endif
-    /* the late-issue (http) kernel frames requests from their header lines
-     * right after the walk: those lines must still be in L2, so its windows
-     * are never non-temporal */
-    const bool nt = (!LATE || RHP_LATE_NT) && !__builtin_amdgcn_ballot_w64(!aligned);
+    const bool nt = !__builtin_amdgcn_ballot_w64(!aligned);
     /* one branch per issue, not one per load (the cache policy is an immediate) */
 #define RHP_ISSUE_LOADS(AUX)                                                                             \
     _Pragma("unroll") for (int i = 0; i < (int) kParts; i++) {                                           \
@@ -825,6 +911,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   for (uint32_t k = tid; k < kPoolWords + kOrderSpan / 32; k += WAVES * 64)
     reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave)[k] = k == 0 ? first_n : 0u;
   wait_vm0();   /* the pending offsets */
+#ifdef RHP_STAMPS
+  const unsigned long long rt_loads = __builtin_amdgcn_s_memrealtime();
+#endif
   const bool uneven =
       may_order && __builtin_amdgcn_ballot_w64((uint64_t) (s1 - s0) * span_n > 2u * (o_hi - o_lo)) != 0;
   if (uneven) {
@@ -939,12 +1028,19 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
        * ready (its offsets landed meanwhile), so a lane never idles an
        * iteration between two requests */
       (void) any_dec;
+#ifdef RHP_STAMPS
+      RHP_STAMP(t1); acc[1] += t1 - t0; t0 = t1;
+#endif
 #pragma unroll
       for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
       if (any_walk) {
         if (!walking) st = kPark;
         walk();
       }
+#ifdef RHP_STAMPS
+      wait_lgkm0();
+      RHP_STAMP(t1); acc[3] += t1 - t0; t0 = t1;
+#endif
       if (walking && wnew) {
         dcur = wcur;
         dlen = wlen;
@@ -952,6 +1048,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         kn = me = pe = rl = nh = ls = t = pco = ovf = 0;
         cand = wget;
         crec_lo = crec_hi = 0;
+        fr = 0;
+        fv = 0;
       }
       dhas = walking;
       dpos = wpos;
@@ -959,13 +1057,20 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #pragma unroll
       for (int w = 0; w < (int) kEvWords; w++) evp[w] = ev[w];
       decode_begin();
+      const uint32_t crec_before = crec_lo | (cand & 0xbfffffffu);
       if (any_walk) decode_window();
+      if (http && any_walk) frame_window(crec_before);
       const bool done = any_walk ? decode_end() : false;
+#ifdef RHP_STAMPS
+      wait_lgkm0();
+      RHP_STAMP(t1); acc[2] += t1 - t0; t0 = t1;
+#endif
       /* the walk of wcur ends with this window: finalized (a terminal, a
        * max_headers stop), or its last byte */
       if (walking && (done || is_done2(st) || is_err2(st) || is_slow2(st) ||
                       (uint32_t) (wpos + (int32_t) kBlock) >= wlen))
         wact = false;
+      /* [E] (the decode above read the staging buffer the issue refills) */
       nw = 0;
       if (walking && wact) nw = (cur_ptr + kBlock) | 1u;
       else if (pend_ok) nw = ((pend_o0 & ~3u) - (uint32_t) base) | 2u;
@@ -974,7 +1079,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     }
 #ifdef RHP_STAMPS
     wait_lgkm0();
-    RHP_STAMP(t1); acc[3] += t1 - t0; t0 = t1;
+    RHP_STAMP(t1); acc[LATE ? 4 : 3] += t1 - t0; t0 = t1;
 #endif
     /* [G] */
     if constexpr (!LATE) {
@@ -1018,6 +1123,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     g_stamps[w * kStampSlots + 11] = n_idle;
     g_stamps[w * kStampSlots + 12] = n_idle_live;
     g_stamps[w * kStampSlots + 13] = n_dry;
+    g_stamps[w * kStampSlots + 19] = rt_loads;
   }
 #endif
 #ifdef RHP_CLOCK
@@ -1206,19 +1312,9 @@ int dfa_waves()   /* RHP_WAVES (experiments): waves per workgroup */
   }();
   return w;
 }
-/* RHP_LATE (A/B): 0 the early window issue everywhere, 1 late issue in http
- * mode, 2 late issue in both modes */
-#ifndef RHP_LATE_DEFAULT
-#define RHP_LATE_DEFAULT 1
-#endif
-bool late_issue(uint32_t mode)
-{
-  static const int l = [] {
-    const char *e = getenv("RHP_LATE");
-    return e ? atoi(e) : RHP_LATE_DEFAULT;
-  }();
-  return l >= 2 || (l == 1 && mode == RHP_MODE_HTTP);
-}
+/* the late-issue form: http mode (frames requests in the loop), or on request
+ * (RHP_IMPL_DFA_LATE, parity tests of that form in phr mode) */
+bool late_issue(uint32_t mode) { return t_impl == RHP_IMPL_DFA_LATE || mode == RHP_MODE_HTTP; }
 }  // namespace
 
 extern "C" {
@@ -1244,7 +1340,7 @@ const char *rhp_kernel_name(void) { return t_impl == RHP_IMPL_EXACT ? "rhp_exact
 
 int rhp_set_impl(int impl)
 {
-  if (impl != RHP_IMPL_DFA && impl != RHP_IMPL_EXACT) return -22;
+  if (impl != RHP_IMPL_DFA && impl != RHP_IMPL_EXACT && impl != RHP_IMPL_DFA_LATE) return -22;
   t_impl = impl;
   return 0;
 }

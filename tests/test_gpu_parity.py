@@ -28,7 +28,9 @@ def golden(name):
 
 
 @pytest.mark.parametrize("impl,layout", [(rhp.IMPL_DFA, rhp.LAYOUT_REQUEST_MAJOR), (rhp.IMPL_EXACT, rhp.LAYOUT_REQUEST_MAJOR),
-                                         (rhp.IMPL_DFA, rhp.LAYOUT_HEADER_MAJOR), (rhp.IMPL_EXACT, rhp.LAYOUT_HEADER_MAJOR)])
+                                         (rhp.IMPL_DFA, rhp.LAYOUT_HEADER_MAJOR), (rhp.IMPL_EXACT, rhp.LAYOUT_HEADER_MAJOR),
+                                         (rhp.IMPL_DFA_LATE, rhp.LAYOUT_REQUEST_MAJOR),
+                                         (rhp.IMPL_DFA_LATE, rhp.LAYOUT_HEADER_MAJOR)])
 @pytest.mark.parametrize("name", sorted(MANIFEST))
 def test_gpu_matches_reference_golden(name, impl, layout):
     spec, buf, off, want, z = golden(name)
@@ -51,9 +53,11 @@ def test_gpu_reference_http_vectors():
 
 @pytest.mark.parametrize("maxh", [0, 1, 3, 16, 32, 64])
 def test_gpu_fuzz_vs_oracle(maxh):
-    for cfg, mode, seed in ((rhp.GEN_FUZZ, rhp.MODE_PHR, 9000 + maxh), (rhp.GEN_FUZZ_HTTP, rhp.MODE_HTTP, 9100 + maxh)):
+    for cfg, mode, seed, impl in ((rhp.GEN_FUZZ, rhp.MODE_PHR, 9000 + maxh, rhp.IMPL_DFA),
+                                  (rhp.GEN_FUZZ, rhp.MODE_PHR, 9200 + maxh, rhp.IMPL_DFA_LATE),
+                                  (rhp.GEN_FUZZ_HTTP, rhp.MODE_HTTP, 9100 + maxh, rhp.IMPL_DFA)):
         buf, off = rhp.generate(cfg, 60000, seed)
-        res = rhp.parse_batch(buf, off, maxh, mode)
+        res = rhp.parse_batch(buf, off, maxh, mode, impl=impl)
         want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
         assert_same(canon(res, mode), want, buf, off, f"GPU fuzz cfg{cfg} maxh{maxh}")
         # the kernel takes the exact path for exactly the requests the emulator of

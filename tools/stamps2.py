@@ -7,10 +7,12 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import libreactorng_amd as rhp
-SLOTS = 20
+SLOTS = 24
 lib = rhp.lib()
 lib.rhp_debug_stamps.argtypes = [ctypes.c_void_p]
-names = ["A wait window", "C-E switch/refill/issue", "decode", "walk", "finalize/handover"]
+# section names: early-issue kernel (phr mode) / late-issue kernel (http mode)
+names = ["A wait window / + framing finish", "C-E switch/refill/issue / C-D switch/refill",
+         "decode / decode + finalize", "walk", "finalize/handover / issue"]
 for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, 1), (rhp.GEN_ZIPF, 0x5EED0003, 32, 0, 0),
                                       (rhp.GEN_POST1K, 0x5EED0005, 16, 1, 1)):
     buf, off = rhp.generate(cfg, 1 << 20, seed)
@@ -44,6 +46,8 @@ for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, 1), (r
     print("   timeline us from the first entry (min / median / p99 / max):")
     print(f"     entry       {q(rt[:, 0])}")
     print(f"     loop start  {q(rt[:, 1])}   prologue {q(rt[:, 1] - rt[:, 0])}")
+    ld = st[used, 19] * 10.0 / 1000.0 - t0
+    print(f"     prologue loads landed {q(ld)}   entry->loads {q(ld - rt[:, 0])}   loads->loop start {q(rt[:, 1] - ld)}")
     print(f"     loop end    {q(rt[:, 2])}   loop     {q(rt[:, 2] - rt[:, 1])}")
     print(f"     exit        {q(rt[:, 3])}   barrier  {q(rt[:, 4] - rt[:, 2])}   replay {q(rt[:, 3] - rt[:, 4])}")
     # by wave slot in the workgroup (dispatch age): iterations and loop end

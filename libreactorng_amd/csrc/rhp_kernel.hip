@@ -635,92 +635,113 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #pragma unroll
     for (int q = 0; q < (int) kEvWords; q++) word(mq[q], (uint32_t) dpos + 32u * (uint32_t) q);
   };
-  /* byte at request position x of the decoded window (dpos <= x < dpos + 128),
-   * from the staging buffer (late-issue kernel: the decode runs before the
-   * issue that refills it) */
-  auto win_byte = [&](uint32_t x) __attribute__((always_inline)) {
-    const uint32_t b = x - (uint32_t) dpos;
-    return lds_u8(stage + stage_off(lane, b >> 4) + (b & 15u));
-  };
-  /* case-insensitive name check against a lower-case literal (OR 0x20: the
-   * one non-letter, '-', could only collide with CR, which no name holds) */
-  auto win_name_is = [&](uint32_t at, auto lit) __attribute__((always_inline)) {
-    constexpr uint32_t n = sizeof(lit.s) - 1;
-    uint32_t c[n], diff = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < n; j++) c[j] = win_byte(at + j);   /* all reads first */
-#pragma unroll
-    for (uint32_t j = 0; j < n; j++) diff |= (c[j] | 0x20u) ^ (uint32_t) (uint8_t) lit.s[j];
-    return diff == 0;
-  };
-  /* strtoull (rhp_scalar.h num_step) over value bytes [from, to) of the
-   * window: the value of a fast-path record starts with neither OWS nor a
-   * CTL, so only the sign and the digit run matter */
-  auto win_number = [&](uint32_t from, uint32_t to) __attribute__((always_inline)) {
-    for (uint32_t x = from; x < to && !(fr & kFrStop); x += 4) {
-      uint32_t c4[4];
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++) c4[k] = win_byte(min(x + k, to - 1u));   /* four reads, one wait */
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++) {
-        if (x + k >= to || (fr & kFrStop)) break;
-        const uint32_t c = c4[k], d = c - '0';
-        const uint32_t cnt = ((fr >> kFrCountSh) & 0xffu) + 1u;
-        fr = (fr & ~(0xffu << kFrCountSh)) | (min(cnt, 255u) << kFrCountSh);
-        if (!(fr & kFrDigits) && (c == '+' || c == '-')) {
-          fr |= kFrDigits | (c == '-' ? kFrNeg : 0u);
-        } else if (d < 10u) {
-          fr |= kFrDigits;
-          fv = fv * 10u + d;
-        } else {
-          fr |= kFrStop;
-        }
-      }
-    }
-  };
-  /* the framing candidate's evaluation after a window's decode (see fr) */
+  /* The framing candidate's evaluation after a window's decode (see fr).  A
+   * lane that needs bytes reads the 36 bytes from one position r of the
+   * window at once (ten aligned ds_read_b32 from the staging buffer, whose
+   * 16-byte parts hold whole dwords): a fresh candidate's name (compared
+   * with both names) and its value from r + 16 (the one SP after the colon),
+   * or the continuation of a Content-Length value from r. */
   auto frame_window = [&](uint32_t crec_before) __attribute__((always_inline)) {
-    if (fr & kFrDefer) return;
     const uint32_t wend = (uint32_t) dpos + kBlock;
-    if ((crec_lo | (cand & 0xbfffffffu)) != crec_before && (cand & 0x3fffffffu) != 0 &&
-        ((cand & 0x3fffffffu) & ((cand & 0x3fffffffu) - 1u)) == 0 && !(cand >> 31)) {
-      /* the first candidate's record completed in this window */
-      const uint32_t name_off = crec_lo & 0xffffu, name_len = crec_lo >> 16;
-      const uint32_t value_off = crec_hi & 0xffffu, value_len = crec_hi >> 16;
-      if (fr & kFrCarry) {   /* Content-Length, value started in an earlier window */
-        win_number(max(value_off, (uint32_t) dpos), value_off + value_len);
-        fr = (fr & ~kFrCarry) | (value_len != 0 ? kFrCl : 0u);   /* an empty value is no Content-Length */
+    const uint32_t hdr = cand & 0x3fffffffu;
+    const bool rec_done = (crec_lo | (cand & 0xbfffffffu)) != crec_before && hdr != 0 && (hdr & (hdr - 1u)) == 0 &&
+                          !(cand >> 31);
+    const uint32_t value_len = crec_hi >> 16;
+    bool need = false, fresh = false;
+    uint32_t r = 0, n = 0, nl = 0;
+    if (fr & kFrDefer) {
+    } else if (rec_done) {   /* the first candidate's record completed in this window */
+      const uint32_t name_off = crec_lo & 0xffffu, name_len = crec_lo >> 16, value_off = crec_hi & 0xffffu;
+      if (fr & kFrCarry) {   /* a Content-Length value that started in an earlier window */
+        r = max(value_off, (uint32_t) dpos);
+        n = value_off + value_len - r;
+        need = true;
       } else if (fr & kFrTeName) {
         fr = (fr & ~kFrTeName) | (value_len != 0 ? kFrTe : 0u);
       } else if (fr & kFrNeither) {
-        /* nothing to frame */
       } else if (name_off < (uint32_t) dpos) {
         fr |= kFrDefer;   /* the name began in an earlier window */
-      } else if (name_len == 14u && win_name_is(name_off, LitCl{})) {
-        if (value_len > kFrMaxValue) fr |= kFrDefer;
-        else if (value_len != 0) { win_number(value_off, value_off + value_len); fr |= kFrCl; }
-      } else if (name_len == 17u && win_name_is(name_off, LitTe{})) {
-        fr |= value_len != 0 ? kFrTe : 0u;
+      } else {
+        r = name_off; nl = name_len; n = value_len; fresh = need = true;
       }
-      if ((fr & kFrCl) && ((fr >> kFrCountSh) & 0xffu) > kFrMaxValue) fr |= kFrDefer;
-    } else if (t && (cand & 0xbfffffffu) == 0) {
-      /* the first candidate's line may be open at the window's end */
+    } else if (t && (cand & 0xbfffffffu) == 0) {   /* its line may be open at the window's end */
       const uint32_t nlen = pco - ls;
       if (fr & kFrCarry) {
-        win_number(max(pco + 2u, (uint32_t) dpos), wend);
-        if (((fr >> kFrCountSh) & 0xffu) > kFrMaxValue) fr |= kFrDefer;
+        r = max(pco + 2u, (uint32_t) dpos);
+        n = wend > r ? wend - r : 0u;
+        need = n != 0;
       } else if (!(fr & (kFrTeName | kFrNeither)) && (nlen == 14u || nlen == 17u)) {
         if (ls < (uint32_t) dpos) {
           fr |= kFrDefer;
-        } else if (nlen == 14u && win_name_is(ls, LitCl{})) {
-          fr |= kFrCarry;
-          win_number(pco + 2u, wend);
-        } else if (nlen == 17u && win_name_is(ls, LitTe{})) {
-          fr |= kFrTeName;
         } else {
-          fr |= kFrNeither;
+          r = ls; nl = nlen; n = wend > ls + 16u ? wend - ls - 16u : 0u; fresh = need = true;
         }
       }
+    }
+    if (!__builtin_amdgcn_ballot_w64(need)) return;
+    if (!need) return;
+    uint32_t raw[10], d[9];
+    const uint32_t b0 = (r - (uint32_t) dpos) & ~3u, sh = (r - (uint32_t) dpos) & 3u;
+#pragma unroll
+    for (uint32_t k = 0; k < 10; k++) {   /* bytes past the window wrap inside the lane's slot: never used */
+      const uint32_t b = b0 + 4u * k;
+      raw[k] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(
+          (size_t) (stage + stage_off(lane, (b >> 4) & 7u) + (b & 15u)));
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 9; k++) d[k] = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh);
+    bool digits = !fresh;
+    if (fresh) {
+      /* case-insensitive compares (OR 0x20: the one non-letter, '-', could
+       * only collide with CR, which no name holds) */
+      uint32_t dcl = 0, dte = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < 17; j++) {
+        const uint32_t c = RHP_BYTE(d, j) | 0x20u;
+        if (j < 14) dcl |= c ^ (uint32_t) (uint8_t) LitCl::s[j];
+        dte |= c ^ (uint32_t) (uint8_t) LitTe::s[j];
+      }
+      if (nl == 14u && dcl == 0) {
+        if (rec_done) {
+          if (value_len > kFrMaxValue) fr |= kFrDefer;
+          else if (value_len != 0) { fr |= kFrCl; digits = true; }
+        } else {
+          fr |= kFrCarry;
+          digits = true;
+        }
+      } else if (nl == 17u && dte == 0) {
+        if (rec_done) fr |= value_len != 0 ? kFrTe : 0u;
+        else fr |= kFrTeName;
+      } else if (!rec_done) {
+        fr |= kFrNeither;
+      }
+    } else if (rec_done) {
+      fr = (fr & ~kFrCarry) | (value_len != 0 ? kFrCl : 0u);   /* an empty value is no Content-Length */
+    }
+    if (digits) {
+      /* strtoull (rhp_scalar.h num_step) over the value bytes: a fast-path
+       * value starts with neither OWS nor a CTL, so only the sign and the
+       * digit run matter; up to 12 bytes per window here, more -> the replay */
+      uint32_t v5[4];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) v5[k] = fresh ? d[4 + k] : d[k];
+      const uint32_t m = min(n, 12u);
+#pragma unroll
+      for (uint32_t j = 0; j < 12; j++) {
+        if (j < m && !(fr & kFrStop)) {
+          const uint32_t c = RHP_BYTE(v5, j), dg = c - '0';
+          fr += 1u << kFrCountSh;
+          if (!(fr & kFrDigits) && (c == '+' || c == '-')) {
+            fr |= kFrDigits | (c == '-' ? kFrNeg : 0u);
+          } else if (dg < 10u) {
+            fr |= kFrDigits;
+            fv = fv * 10u + dg;
+          } else {
+            fr |= kFrStop;
+          }
+        }
+      }
+      if ((n > 12u && !(fr & kFrStop)) || ((fr >> kFrCountSh) & 0xffu) > kFrMaxValue) fr |= kFrDefer;
     }
   };
   /* set up the decode of the window walked last iteration */
@@ -842,6 +863,38 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     uint32_t c[8], r[8];
     codes_a(W[0], r);
     codes_b(W[0], r, c);
+#ifndef RHP_WALK_INTERLEAVE
+#define RHP_WALK_INTERLEAVE 1
+#endif
+#if RHP_WALK_INTERLEAVE
+    /* Each chained step's read is followed by one independent lookup for the
+     * next part (its class-row read, and the code read of the step before,
+     * whose class row has landed by then): in-order LDS returns, so the step
+     * waits only for its own read while the lookups fly behind it, instead of
+     * queueing behind eight of them at the head of each group of four. */
+#pragma unroll
+    for (int q = 0; q < (int) kParts; q++) {
+      const bool nx = q + 1 < (int) kParts;
+      uint32_t cn[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        st = lds_u8(__builtin_amdgcn_perm(st, c[j], 0x0c0c0400u));
+        __builtin_amdgcn_sched_barrier(0);   /* the chained read issues first */
+        if (nx)
+          r[j] = lds_u8(__builtin_amdgcn_perm(kClassRowR, W[q + 1][j >> 1], 0x0c0c0400u | (uint32_t) (2 * (j & 1) + 1)));
+        if (nx && j > 0)
+          cn[j - 1] = lds_u8(__builtin_amdgcn_perm(r[j - 1], W[q + 1][(j - 1) >> 1], 0x0c0c0400u | (uint32_t) (2 * ((j - 1) & 1))));
+        __builtin_amdgcn_sched_barrier(0);
+        ev_shift2(ev[q >> 1], st);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (nx) {
+        cn[7] = lds_u8(__builtin_amdgcn_perm(r[7], W[q + 1][3], 0x0c0c0400u | 2u));
+#pragma unroll
+        for (int j = 0; j < 8; j++) c[j] = cn[j];
+      }
+    }
+#else
 #pragma unroll
     for (int q = 0; q < (int) kParts; q++) {
       uint32_t cn[8];
@@ -859,6 +912,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         for (int j = 0; j < 8; j++) c[j] = cn[j];
       }
     }
+#endif
   };
 
   /* LDS-DMA of every lane's next window (nw) into the staging buffer:

@@ -265,10 +265,6 @@ __device__ __forceinline__ bool http_frame_fast(const uint8_t *b, uint64_t len, 
   return true;
 }
 
-/* the framing names as types (compile-time literals for the LDS compare) */
-struct LitCl { static constexpr char s[] = "content-length"; };
-struct LitTe { static constexpr char s[] = "transfer-encoding"; };
-
 /* Params pointers are generic in the kernel's view (they sit in a struct);
  * the hot stores go through explicit global-address-space pointers so they are
  * global_store (VM counter only), not flat_store (VM + LGKM). */
@@ -694,13 +690,18 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     if (fresh) {
       /* case-insensitive compares (OR 0x20: the one non-letter, '-', could
        * only collide with CR, which no name holds) */
+      /* "content-length", "transfer-encoding" as little-endian dwords */
+      constexpr uint32_t kCl[3] = {0x746e6f63u, 0x2d746e65u, 0x676e656cu};
+      constexpr uint32_t kTe[4] = {0x6e617274u, 0x72656673u, 0x636e652du, 0x6e69646fu};
       uint32_t dcl = 0, dte = 0;
 #pragma unroll
-      for (uint32_t j = 0; j < 17; j++) {
-        const uint32_t c = RHP_BYTE(d, j) | 0x20u;
-        if (j < 14) dcl |= c ^ (uint32_t) (uint8_t) LitCl::s[j];
-        dte |= c ^ (uint32_t) (uint8_t) LitTe::s[j];
+      for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t x = d[k] | 0x20202020u;
+        dte |= x ^ kTe[k];
+        if (k < 3) dcl |= x ^ kCl[k];
       }
+      dcl |= ((d[3] | 0x2020u) ^ ((uint32_t) 'h' << 8 | 't')) & 0xffffu;   /* "th" */
+      dte |= ((d[4] | 0x20u) ^ 'g') & 0xffu;
       if (nl == 14u && dcl == 0) {
         if (rec_done) {
           if (value_len > kFrMaxValue) fr |= kFrDefer;
@@ -722,14 +723,14 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       /* strtoull (rhp_scalar.h num_step) over the value bytes: a fast-path
        * value starts with neither OWS nor a CTL, so only the sign and the
        * digit run matter; up to 12 bytes per window here, more -> the replay */
-      uint32_t v5[4];
+      uint32_t v5[3];
 #pragma unroll
-      for (uint32_t k = 0; k < 4; k++) v5[k] = fresh ? d[4 + k] : d[k];
+      for (uint32_t k = 0; k < 3; k++) v5[k] = fresh ? d[4 + k] : d[k];
       const uint32_t m = min(n, 12u);
-#pragma unroll
-      for (uint32_t j = 0; j < 12; j++) {
+      for (uint32_t j = 0; __builtin_amdgcn_ballot_w64(j < m && !(fr & kFrStop)); j++) {
         if (j < m && !(fr & kFrStop)) {
-          const uint32_t c = RHP_BYTE(v5, j), dg = c - '0';
+          const uint32_t w = j < 4u ? v5[0] : j < 8u ? v5[1] : v5[2];
+          const uint32_t c = (w >> (8u * (j & 3u))) & 0xffu, dg = c - '0';
           fr += 1u << kFrCountSh;
           if (!(fr & kFrDigits) && (c == '+' || c == '-')) {
             fr |= kFrDigits | (c == '-' ? kFrNeg : 0u);
@@ -1008,7 +1009,19 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   const unsigned long long rt_loop = __builtin_amdgcn_s_memrealtime();
   unsigned long long n_walk = 0, n_idle = 0, n_idle_live = 0, n_dry = 0;
 #endif
+  /* The SIMD issues by priority, then age: with equal priorities the waves
+   * dispatched last in a workgroup run slowest and finish its range last.
+   * Rotating every wave's priority each iteration (phase by wave) shares the
+   * issue slots evenly (config 2 -1 %, configs 3 and 5 -3 %). */
+  uint32_t prio_it = (tid >> 6) & 3u;
   for (;;) {
+    prio_it = (prio_it + 1u) & 3u;
+    switch (prio_it) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3);
+    }
     RHP_STAMP(t0);
     /* [A] */
     wait_vm0();   /* the window's LDS-DMA has landed (and the pending offsets, and older stores) */

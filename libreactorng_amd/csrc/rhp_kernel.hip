@@ -345,7 +345,7 @@ __device__ __forceinline__ void store_http_bad(rhp_http_t *dst)
  * events of the window walked in the previous iteration) -- the same request
  * unless the lane switched between the two windows.
  */
-template <int WAVES, bool LATE>
+template <int WAVES, bool LATE, bool HTTP>
 __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel(Params p)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #endif
 
   const uint32_t maxh = p.max_headers;
-  const bool http = p.mode == RHP_MODE_HTTP;
+  constexpr bool http = HTTP;   /* p.mode == RHP_MODE_HTTP (the launch picks the instance) */
 
   /* ---- request pool ----
    * Workgroup g owns requests [g*span, (g+1)*span) (host: span = n / grid).
@@ -385,6 +385,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   uint16_t *long_list = reinterpret_cast<uint16_t *>(long_bits + kOrderSpan / 32);
   const bool order_on = wg_hi - wg_lo <= kOrderSpan;
   bool list_dry = !order_on;
+  bool listed = false;   /* the range was scanned: skip the listed requests in order */
   bool first_iter = true;   /* the list is complete only after the scan (before the loop) */
   bool pool_dry = wg_lo >= wg_hi;
   /* The prologue's global reads all go out at once (one round trip): the
@@ -481,7 +482,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (b0 + cnt >= wg_hi) pool_dry = true;
       const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
       const uint32_t i = b0 + rank, k = i - wg_lo;
-      if (!pend_ok && i < wg_hi && !(order_on && ((long_bits[k >> 5] >> (k & 31)) & 1u))) take(i);
+      if (!pend_ok && i < wg_hi && !(listed && ((long_bits[k >> 5] >> (k & 31)) & 1u))) take(i);
       want = __ballot(!pend_ok);
     }
   };
@@ -978,6 +979,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
      * before the scan; the list complete and the counter reset before the
      * first refill) */
     pend_ok = false;
+    listed = true;
     __syncthreads();
     if (tid == 0) *wg_counter = 0;
     scan_long();
@@ -994,6 +996,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     issue();
     __syncthreads();
     first_iter = false;
+    list_dry = true;   /* nothing listed: refills take the range in order */
   }
 
   /*
@@ -1075,7 +1078,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #endif
       /* [F] walk + decode of the previous window */
       decode_begin();
+#ifndef RHP_EXP_NODECODE
       if (any_dec) decode_window();
+#endif
 #pragma unroll
       for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
 #ifdef RHP_STAMPS
@@ -1333,7 +1338,7 @@ namespace {
  * the implementation choice (rhp_set_impl, diagnostics) is per thread. */
 constexpr int kMaxDevices = 64;
 std::atomic<int> g_cus[kMaxDevices];
-std::atomic<uint32_t> g_attr[kMaxDevices];   /* bit 2(w/4)+late: the LDS attribute of rhp_dfa_kernel<w, late> is set */
+std::atomic<uint32_t> g_attr[kMaxDevices];   /* bit 4(w/4)+2late+http: the LDS attribute of rhp_dfa_kernel<w, late, http> is set */
 thread_local int t_impl = RHP_IMPL_DFA;
 
 int device_cus(int dev, int *cus)
@@ -1348,14 +1353,14 @@ int device_cus(int dev, int *cus)
   return 0;
 }
 
-template <int WAVES, bool LATE>
+template <int WAVES, bool LATE, bool HTTP>
 int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
 {
   const size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes;
-  const uint32_t bit = 1u << (2 * (WAVES / 4) + (LATE ? 1 : 0));
+  const uint32_t bit = 1u << (4 * (WAVES / 4) + (LATE ? 2 : 0) + (HTTP ? 1 : 0));
   if (!(g_attr[dev].load(std::memory_order_acquire) & bit)) {
     /* idempotent: two threads of one device may both set it */
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES, LATE>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES, LATE, HTTP>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds_bytes);
     if (e != hipSuccess) return (int) e;
     g_attr[dev].fetch_or(bit, std::memory_order_release);
@@ -1367,7 +1372,7 @@ int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
   /* each workgroup owns a contiguous n/grid share of the requests */
   Params q = prm;
   q.span = (prm.n + grid - 1) / grid;
-  hipLaunchKernelGGL((rhp_dfa_kernel<WAVES, LATE>), dim3(grid), dim3(WAVES * 64), lds_bytes, s, q);
+  hipLaunchKernelGGL((rhp_dfa_kernel<WAVES, LATE, HTTP>), dim3(grid), dim3(WAVES * 64), lds_bytes, s, q);
   return (int) hipGetLastError();
 }
 
@@ -1458,11 +1463,12 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
     return (int) hipGetLastError();
   }
   const bool late = late_issue(b->mode);
-  if (late) return launch_dfa<16, true>(prm, s, dev, cus);
+  if (b->mode == RHP_MODE_HTTP) return launch_dfa<16, true, true>(prm, s, dev, cus);
+  if (late) return launch_dfa<16, true, false>(prm, s, dev, cus);
   switch (dfa_waves()) {
-  case 8: return launch_dfa<8, false>(prm, s, dev, cus);
-  case 12: return launch_dfa<12, false>(prm, s, dev, cus);
-  default: return launch_dfa<16, false>(prm, s, dev, cus);
+  case 8: return launch_dfa<8, false, false>(prm, s, dev, cus);
+  case 12: return launch_dfa<12, false, false>(prm, s, dev, cus);
+  default: return launch_dfa<16, false, false>(prm, s, dev, cus);
   }
 }
 

@@ -851,29 +851,16 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     for (int j = 0; j < 8; j++)
       c[j] = lds_u8(__builtin_amdgcn_perm(r[j], chunk[j >> 1], 0x0c0c0400u | (uint32_t) (2 * (j & 1))));
   };
-  auto steps4 = [&](const uint32_t (&c)[8], int j0, uint32_t &e) {
-#pragma unroll
-    for (int j = j0; j < j0 + 4; j++) {
-      st = lds_u8(__builtin_amdgcn_perm(st, c[j], 0x0c0c0400u));
-      ev_shift2(e, st);
-    }
-  };
-  /* the walk of the window in W, with the decode slots of the previous window
-   * between its groups of four chained steps: chunk q+1's first lookups are
-   * issued before chunk q's chain, its second ones after half the chain */
+  /* The walk of the window in W: part 0's codes first, then per chained step
+   * one independent lookup pair for the next part behind the step's read (its
+   * class-row read, and the code read of the step before, whose class row has
+   * landed by then).  LDS returns in order, so a step waits only for its own
+   * read while the lookups fly behind it (issued ahead of it, a batch of eight
+   * delayed every fourth step: config 2 +3 %). */
   auto walk = [&]() {
     uint32_t c[8], r[8];
     codes_a(W[0], r);
     codes_b(W[0], r, c);
-#ifndef RHP_WALK_INTERLEAVE
-#define RHP_WALK_INTERLEAVE 1
-#endif
-#if RHP_WALK_INTERLEAVE
-    /* Each chained step's read is followed by one independent lookup for the
-     * next part (its class-row read, and the code read of the step before,
-     * whose class row has landed by then): in-order LDS returns, so the step
-     * waits only for its own read while the lookups fly behind it, instead of
-     * queueing behind eight of them at the head of each group of four. */
 #pragma unroll
     for (int q = 0; q < (int) kParts; q++) {
       const bool nx = q + 1 < (int) kParts;
@@ -896,25 +883,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         for (int j = 0; j < 8; j++) c[j] = cn[j];
       }
     }
-#else
-#pragma unroll
-    for (int q = 0; q < (int) kParts; q++) {
-      uint32_t cn[8];
-      if (q + 1 < (int) kParts) codes_a(W[q + 1], r);
-      __builtin_amdgcn_sched_barrier(0);
-      steps4(c, 0, ev[q >> 1]);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (q + 1 < (int) kParts) codes_b(W[q + 1], r, cn);
-      __builtin_amdgcn_sched_barrier(0);
-      steps4(c, 4, ev[q >> 1]);
-      __builtin_amdgcn_sched_barrier(0);
-      if (q + 1 < (int) kParts) {
-#pragma unroll
-        for (int j = 0; j < 8; j++) c[j] = cn[j];
-      }
-    }
-#endif
   };
 
   /* LDS-DMA of every lane's next window (nw) into the staging buffer:
@@ -1078,9 +1046,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #endif
       /* [F] walk + decode of the previous window */
       decode_begin();
-#ifndef RHP_EXP_NODECODE
       if (any_dec) decode_window();
-#endif
 #pragma unroll
       for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
 #ifdef RHP_STAMPS

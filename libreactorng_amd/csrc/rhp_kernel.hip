@@ -976,7 +976,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * decoded request if it ended, hand the decode over to the walked window.
    */
 #ifdef RHP_STAMPS
-  unsigned long long t0 = 0, t1 = 0, acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long t0 = 0, t1 = 0, acc[6] = {0, 0, 0, 0, 0, 0}, acc_dw = 0, acc_fw = 0;
   const unsigned long long rt_loop = __builtin_amdgcn_s_memrealtime();
   unsigned long long n_walk = 0, n_idle = 0, n_idle_live = 0, n_dry = 0;
 #endif
@@ -1097,7 +1097,13 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       decode_begin();
       const uint32_t crec_before = crec_lo | (cand & 0xbfffffffu);
       if (any_walk) decode_window();
+#ifdef RHP_STAMPS
+      wait_lgkm0(); RHP_STAMP(t1); acc_dw += t1 - t0; t0 = t1;
+#endif
       if (http && any_walk) frame_window(crec_before);
+#ifdef RHP_STAMPS
+      wait_lgkm0(); RHP_STAMP(t1); acc_fw += t1 - t0; t0 = t1;
+#endif
       const bool done = any_walk ? decode_end() : false;
 #ifdef RHP_STAMPS
       wait_lgkm0();
@@ -1162,6 +1168,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     g_stamps[w * kStampSlots + 12] = n_idle_live;
     g_stamps[w * kStampSlots + 13] = n_dry;
     g_stamps[w * kStampSlots + 19] = rt_loads;
+    g_stamps[w * kStampSlots + 20] = acc_dw;   /* late form: decode_window cycles (within section 2) */
+    g_stamps[w * kStampSlots + 21] = acc_fw;   /* late form: frame_window cycles (within section 2) */
   }
 #endif
 #ifdef RHP_CLOCK

@@ -34,8 +34,9 @@
  * byte lies before `len`; constructs that are rare in real traffic or whose
  * answer depends on where the buffer ends go to the SLOW terminal and are
  * re-parsed by the exact scalar path (rhp_scalar.h): a leading empty line, an
- * empty method, more than one SP between request-line fields, versions other
- * than HTTP/1.0 and HTTP/1.1, bare-LF line ends, anything but exactly one SP
+ * empty method, more than one SP between request-line fields, minor versions
+ * other than 0 and 1 (a version that is not "HTTP/1." + digit is ERR, trusted
+ * when the version's 9 bytes are in the buffer), bare-LF line ends, anything but exactly one SP
  * after a header colon (":v", ":\tv", ":  v", ":\r\n"), OWS before a CR
  * (value trimming), obs-fold continuation lines.  A header section longer
  * than the u16 records hold (ret > RHP_MAX_LEN) is also handed to the exact
@@ -126,15 +127,20 @@ constexpr uint32_t step(uint32_t s, uint32_t c)
   case S_PATH:
     if (c == ' ') return S_SP2_E;
     return c_ctl(c) ? S_ERR_E : S_PATH;
-  case S_SP2_E:     /* "HTTP/1." + digit (:245-261) right after one SP */
-    return c == 'H' ? S_V1 : S_SLOW;
-  case S_V1: return c == 'T' ? S_V2 : S_SLOW;
-  case S_V2: return c == 'T' ? S_V3 : S_SLOW;
-  case S_V3: return c == 'P' ? S_V4 : S_SLOW;
-  case S_V4: return c == '/' ? S_V5 : S_SLOW;
-  case S_V5: return c == '1' ? S_V6 : S_SLOW;
-  case S_V6: return c == '.' ? S_V7 : S_SLOW;
-  case S_V7: return c == '0' ? S_V8_0 : c == '1' ? S_V8_1 : S_SLOW;
+  case S_SP2_E:     /* "HTTP/1." + digit (:245-261) right after one SP (a second SP is
+                       skipped by :360-362: exact path) */
+    return c == 'H' ? S_V1 : c == ' ' ? S_SLOW : S_ERR_E;
+  /* a mismatch in the version is -1 (EXPECT_CHAR_NO_CHECK, :252-258) when the
+   * 9 bytes of the version are there (:248-251): finalize trusts an ERR before
+   * the request-line end only when len >= PE + 10 (rhp_kernel.hip decode_end) */
+  case S_V1: return c == 'T' ? S_V2 : S_ERR_E;
+  case S_V2: return c == 'T' ? S_V3 : S_ERR_E;
+  case S_V3: return c == 'P' ? S_V4 : S_ERR_E;
+  case S_V4: return c == '/' ? S_V5 : S_ERR_E;
+  case S_V5: return c == '1' ? S_V6 : S_ERR_E;
+  case S_V6: return c == '.' ? S_V7 : S_ERR_E;
+  case S_V7:        /* PARSE_INT (:259): minors 2-9 (and tchar letters, one class) -> exact path */
+    return c == '0' ? S_V8_0 : c == '1' ? S_V8_1 : c_tchar(c) ? S_SLOW : S_ERR_E;
   case S_V8_0:      /* the request line ends with CRLF (:370-378); bare LF -> exact path */
     if (c == '\r') return S_CRLF_RL_E;
     return c == '\n' ? S_SLOW : S_ERR_E;

@@ -109,7 +109,10 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
       if (!(ovf || slow || term_ev || pos >= (int32_t) len)) continue;
       /* ---- finalize (same decisions as the kernel) ---- */
       const bool ok = !ovf && is_done2(st) && term_pos < len && term_pos < RHP_MAX_LEN;
-      const bool bad = ovf ? d.ovf - 1u < len : (is_err2(st) && term_pos < len);
+      /* an ERR in the version (request line events ME, PE consumed) needs the
+       * version's 9 bytes: len >= PE + 10 (picohttpparser.c:248-251) */
+      const bool bad = ovf ? d.ovf - 1u < len
+                           : (is_err2(st) && term_pos < len && (d.k != 2 || d.e[0] + 10u <= len));
       if (ok) {
         st_count.fast_ok++;
         rhp_req_t r;

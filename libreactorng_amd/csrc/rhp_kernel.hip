@@ -781,7 +781,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const bool fin = dhas && (ovfl || is_slow2(e) || term_ev || (uint32_t) dpos + kBlock >= dlen);
     if (!fin) return false;
     const bool ok = !ovfl && is_done2(e) && term_pos < dlen && term_pos < RHP_MAX_LEN;
-    const bool bad = ovfl ? ovf - 1u < dlen : (is_err2(e) && term_pos < dlen);
+    /* an ERR between the path and the request-line end (the version, kn == 2)
+     * is -1 only when the version's 9 bytes are there (picohttpparser.c:248-251):
+     * len >= PE + 10 */
+    const bool bad = ovfl ? ovf - 1u < dlen
+                          : (is_err2(e) && term_pos < dlen && ((kn & 7u) != 2u || pe + 10u <= dlen));
     /* the record as four dwords (rhp.h rhp_req_t: ret; method_len, path_off;
      * path_len, method_off 0, minor_version; num_headers, flags) */
     u32x4 rq = u32x4{0u, 0u, 0xff000000u, 0u};   /* minor_version -1 */

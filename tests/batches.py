@@ -31,6 +31,18 @@ EDGE = [
 ]
 
 
+def version_batch():
+    """Request lines whose version is not HTTP/1.<digit>, cut at every length: the
+    kernel's DFA answers -1 for them only when the version's 9 bytes are in the
+    buffer (picohttpparser.c:248-258, rhp_dfa.h S_V1..S_V7), else the exact path
+    decides (-2 for a short buffer)."""
+    bases = [b"GET / HTTP/2.0\r\n\r\n", b"GET / HTTX/1.1\r\nA: b\r\n\r\n", b"GET / XTTP/1.1\r\n\r\n",
+             b"GET / HTTP/1.x\r\n\r\n", b"GET / HTTP/1.5\r\n\r\n", b"GET / HTTP/11.1\r\n\r\n",
+             b"GET / http/1.1\r\n\r\n", b"GET /p \r\n\r\n", b"GET /p HTTP/1.1X\r\n\r\n", b"GET /p HTTP/1.\x01\r\n\r\n",
+             b"POST /u HTTP/2.0\r\nContent-Length: 3\r\n\r\nabc", b"GET /p HTTP/1.1\rX\r\n\r\n"]
+    return [b[:k] for b in bases for k in range(len(b) + 1)]
+
+
 def dense_header_batch(n=3000, seed=5):
     """Adversarial: many 3-byte header lines ("a:\n") so up to 6 header records
     start inside one 16-byte check interval (capture-ring wrap, request-line

@@ -170,3 +170,16 @@ def test_dense_headers_emulation(shift):
             res, _ = rhp.emulate(buf, off, maxh, mode)
             want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
             assert_same(canon(res, mode), want, buf, off, f"dense shift{shift} maxh{maxh} mode{mode}")
+
+
+@pytest.mark.parametrize("mode", [rhp.MODE_PHR, rhp.MODE_HTTP])
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+def test_emulator_version_errors_vs_oracle(mode, shift):
+    """A version that is not HTTP/1.<digit> at every cut length: the emulator of
+    the kernel's algorithm (its DFA ERR with the PE + 10 length rule) against the
+    oracle."""
+    from batches import version_batch
+    buf, off = pack(version_batch(), align_shift=shift)
+    emu, _ = rhp.emulate(buf, off, 16, mode)
+    want = to_rhp(*run_oracle(buf, off, 16, mode)[:3], mode)
+    assert_same(canon(emu, mode), want, buf, off, f"emu version mode{mode} shift{shift}")

@@ -178,3 +178,16 @@ def test_gpu_full_size_matches_reference_digest(name):
         want = to_rhp(*run_oracle(buf, off, spec["max_headers"], spec["mode"])[:3], spec["mode"])
         assert_same(got, want, buf, off, name)
         raise AssertionError(f"{name}: digest differs from the reference but matches the oracle")
+
+
+@pytest.mark.parametrize("impl", [rhp.IMPL_DFA, rhp.IMPL_DFA_LATE])
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+def test_gpu_version_errors(impl, shift):
+    """Versions that are not HTTP/1.<digit>, cut at every length (batches.version_batch):
+    -1 from the DFA only when the version's 9 bytes are there, else the exact path."""
+    from batches import version_batch
+    buf, off = pack(version_batch() * 2, align_shift=shift)
+    for mode in (rhp.MODE_PHR, rhp.MODE_HTTP):
+        res = rhp.parse_batch(buf, off, 16, mode, impl=impl)
+        want = to_rhp(*run_oracle(buf, off, 16, mode)[:3], mode)
+        assert_same(canon(res, mode), want, buf, off, f"GPU version impl{impl} shift{shift} mode{mode}")

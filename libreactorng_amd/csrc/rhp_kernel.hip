@@ -944,6 +944,17 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #endif
   const bool uneven =
       may_order && __builtin_amdgcn_ballot_w64((uint64_t) (s1 - s0) * span_n > 2u * (o_hi - o_lo)) != 0;
+  /* An uneven range runs on 12 of the 16 waves: its end is set by its longest
+   * requests (each walked by one lane from the first iteration on), and with
+   * fewer waves sharing the CU every iteration is shorter while the lanes'
+   * share of the rest still fits beside them (config 3: 16 waves 422 us, 12
+   * waves 398 us, 8 waves 474 us).  The other waves only join the barriers and
+   * the replay. */
+#ifndef RHP_UNEVEN_WAVES
+#define RHP_UNEVEN_WAVES 12
+#endif
+  constexpr uint32_t kUnevenWaves = WAVES > RHP_UNEVEN_WAVES ? (uint32_t) RHP_UNEVEN_WAVES : (uint32_t) WAVES;
+  bool idle_wave = false;
   if (uneven) {
     /* every request longer than twice the range's mean is handed out before
      * the others, the first hand-out included: a long request never waits
@@ -952,15 +963,18 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
      * first refill) */
     pend_ok = false;
     listed = true;
+    idle_wave = (tid >> 6) >= kUnevenWaves;
     __syncthreads();
     if (tid == 0) *wg_counter = 0;
     scan_long();
     __syncthreads();
     first_iter = false;
-    refill_pend();
-    wait_vm0();
-    nw = pend_ok ? ((pend_o0 & ~3u) - (uint32_t) base) | 2u : 0u;
-    issue();
+    if (!idle_wave) {
+      refill_pend();
+      wait_vm0();
+      nw = pend_ok ? ((pend_o0 & ~3u) - (uint32_t) base) | 2u : 0u;
+      issue();
+    }
   } else {
     /* the first windows, then the barrier that makes the pool area
      * initialized before any wave's first refill */
@@ -989,7 +1003,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * Rotating every wave's priority each iteration (phase by wave) shares the
    * issue slots evenly (config 2 -1 %, configs 3 and 5 -3 %). */
   uint32_t prio_it = (tid >> 6) & 3u;
-  for (;;) {
+  while (!idle_wave) {
     prio_it = (prio_it + 1u) & 3u;
     switch (prio_it) {
     case 0: __builtin_amdgcn_s_setprio(0); break;

@@ -1,0 +1,166 @@
+// ubench_ceiling.hip -- what one launch of config 2's size (268 MB of request
+// bytes, 48 MB of records written) can reach on gfx950 (MI355X), launched back
+// to back over 4 rotated copies (1 GiB, beyond the 256 MiB Infinity Cache) as
+// bench.py does.  Every kernel reads every byte once (xor-folded), some also
+// write config 2's record bytes (16 B + 4 x 8 B per 256-B request).
+//   coal<U,NT,W>   grid-stride, wave reads 1 KiB per global_load_dwordx4, U in flight
+//   chunk<U,NT,W>  persistent: a workgroup pulls 64 KiB chunks from a global counter
+//   hipcc --offload-arch=gfx950 -O3 tools/ubench_ceiling.hip -o tools/ubench_ceiling
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const u32x4 gq;
+
+constexpr uint64_t kBytes = 268435456ull;   /* 1M x 256 B */
+constexpr uint64_t kReqs = kBytes / 256;
+
+/* the records of request i: 16 B at reqs[i], 4 x 8 B header-major at hdrs[k * n + i] */
+__device__ __forceinline__ void write_records(uint8_t *reqs, uint8_t *hdrs, uint64_t i, uint32_t v)
+{
+  *reinterpret_cast<__attribute__((address_space(1))) u32x4 *>((uintptr_t) (reqs + 16 * i)) = u32x4{v, 1, 2, 3};
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    *reinterpret_cast<__attribute__((address_space(1))) u32x2 *>((uintptr_t) (hdrs + 8 * ((uint64_t) k * kReqs + i))) =
+        u32x2{v, (uint32_t) k};
+}
+
+template <int U, int NT, int W>
+__global__ void coal(const uint8_t *buf, uint8_t *reqs, uint8_t *hdrs, uint32_t *out)
+{
+  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x * 16 * U;
+  uint32_t acc = 0;
+  for (uint64_t at = ((uint64_t) blockIdx.x * blockDim.x * U + threadIdx.x) * 16; at < kBytes; at += stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      gq *p = (gq *) (uintptr_t) (buf + at + (uint64_t) u * blockDim.x * 16);
+      v[u] = NT ? __builtin_nontemporal_load(p) : *p;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+    if (W) {
+      /* one request's records per 16 lanes' worth of bytes: lanes with
+       * (threadIdx & 15) == 0 of the first load write them */
+      const uint64_t b0 = at;   /* this lane's first byte */
+      if ((b0 & 255) == 0) write_records(reqs, hdrs, b0 >> 8, acc);
+#pragma unroll
+      for (int u = 1; u < U; u++) {
+        const uint64_t b = at + (uint64_t) u * blockDim.x * 16;
+        if ((b & 255) == 0) write_records(reqs, hdrs, b >> 8, acc);
+      }
+    }
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
+/* persistent: workgroup pulls CHUNK-byte chunks from a global counter (one
+ * lane, the next chunk prefetched one chunk ahead) */
+template <int U, int NT, int W, uint32_t CHUNK>
+__global__ void chunk(const uint8_t *buf, uint8_t *reqs, uint8_t *hdrs, uint32_t *out, uint32_t *ctr)
+{
+  __shared__ uint32_t next;
+  const uint32_t nchunks = (uint32_t) (kBytes / CHUNK);
+  uint32_t acc = 0;
+  if (threadIdx.x == 0) next = atomicAdd(ctr, 1u);
+  __syncthreads();
+  uint32_t c = next;
+  while (c < nchunks) {
+    __syncthreads();
+    if (threadIdx.x == 0) next = atomicAdd(ctr, 1u);   /* lands while this chunk streams */
+    const uint64_t base = (uint64_t) c * CHUNK;
+    for (uint32_t at = threadIdx.x * 16; at < CHUNK; at += blockDim.x * 16 * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        gq *p = (gq *) (uintptr_t) (buf + base + at + (uint64_t) u * blockDim.x * 16);
+        v[u] = NT ? __builtin_nontemporal_load(p) : *p;
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+      if (W) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint64_t b = base + at + (uint64_t) u * blockDim.x * 16;
+          if ((b & 255) == 0) write_records(reqs, hdrs, b >> 8, acc);
+        }
+      }
+    }
+    __syncthreads();
+    c = next;
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
+struct Bufs {
+  uint8_t *in[4];
+  uint8_t *reqs, *hdrs;
+  uint32_t *out, *ctr;
+};
+
+template <class L>
+void run(const char *name, L launch, Bufs &b, bool counter)
+{
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  const int steps = 50;
+  for (int k = 0; k < 8; k++) {
+    if (counter) CHECK(hipMemsetAsync(b.ctr + 64 * (k % 4), 0, 4));
+    launch(b.in[k % 4], b.ctr + 64 * (k % 4));
+  }
+  CHECK(hipDeviceSynchronize());
+  /* counters for the timed launches are zeroed beforehand (a memset between
+   * launches would be timed too): one counter per launch */
+  if (counter) CHECK(hipMemset(b.ctr, 0, 4 * 64 * steps));
+  CHECK(hipEventRecord(e0));
+  for (int k = 0; k < steps; k++) launch(b.in[k % 4], b.ctr + 64 * k);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = 1e3 * ms / steps;
+  printf("%-34s %7.1f us  %6.0f GB/s read  frac %.3f\n", name, us, kBytes / us / 1e3, kBytes / us / 1e3 / 8000.0);
+  fflush(stdout);
+}
+
+int main()
+{
+  Bufs b;
+  for (int k = 0; k < 4; k++) {
+    CHECK(hipMalloc(&b.in[k], kBytes + 4096));
+    CHECK(hipMemset(b.in[k], k + 1, kBytes + 4096));
+  }
+  CHECK(hipMalloc(&b.reqs, 16 * kReqs));
+  CHECK(hipMalloc(&b.hdrs, 32 * kReqs));
+  CHECK(hipMalloc(&b.out, 4 << 20));
+  CHECK(hipMalloc(&b.ctr, 4 * 64 * 64));
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  printf("CUs %d, %llu B per launch, 4 rotated copies\n", cus, (unsigned long long) kBytes);
+#define COAL(U, NT, W, GRID, BLOCK)                                                                               \
+  run("coal U" #U " nt" #NT " w" #W " grid " #GRID "x" #BLOCK,                                                  \
+      [&](uint8_t *in, uint32_t *) { hipLaunchKernelGGL((coal<U, NT, W>), dim3(GRID), dim3(BLOCK), 0, 0, in, b.reqs, b.hdrs, b.out); }, b, false)
+#define CHUNK(U, NT, W, C, GRID, BLOCK)                                                                            \
+  run("chunk" #C " U" #U " nt" #NT " w" #W " grid " #GRID "x" #BLOCK,                                            \
+      [&](uint8_t *in, uint32_t *ctr) { hipLaunchKernelGGL((chunk<U, NT, W, C>), dim3(GRID), dim3(BLOCK), 0, 0, in, b.reqs, b.hdrs, b.out, ctr); }, b, true)
+  for (int rep = 0; rep < 2; rep++) {
+    COAL(4, 1, 0, 256 * 4, 256);
+    COAL(4, 1, 0, 256, 1024);
+    COAL(8, 1, 0, 256, 1024);
+    COAL(4, 0, 0, 256, 1024);
+    COAL(4, 1, 0, 256 * 16, 256);
+    COAL(4, 1, 1, 256, 1024);
+    COAL(4, 1, 1, 256 * 4, 256);
+    CHUNK(4, 1, 0, 65536, 256, 1024);
+    CHUNK(4, 1, 0, 16384, 256, 1024);
+    CHUNK(4, 1, 0, 16384, 512, 512);
+    CHUNK(4, 1, 1, 65536, 256, 1024);
+    CHUNK(4, 1, 1, 16384, 512, 512);
+  }
+  return 0;
+}

@@ -111,6 +111,12 @@ typedef struct rhp_batch {
   uint32_t       *work;        /* reserved, may be NULL (device scratch of RHP_WORK_WORDS u32
                                   for future kernels; the current ones keep their scheduling
                                   state in LDS) */
+  const uint64_t *last_len;    /* device [n] or NULL (= all 0), RHP_MODE_PHR only:
+                                  phr_parse_request's last_len per request
+                                  (picohttpparser.c:383, 399-401): when last_len[i] != 0 the
+                                  slowloris pre-check is_complete (:197-223) runs first and
+                                  its -2 / -1 is the answer.  Contract: last_len[i] <= len
+                                  (the reference reads before `buf_end` only then) */
 } rhp_batch_t;
 
 #define RHP_WORK_WORDS 64u

@@ -48,7 +48,8 @@ class Batch(ctypes.Structure):
     _fields_ = [("bytes", ctypes.c_void_p), ("bytes_rw", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
                 ("bytes_size", ctypes.c_uint64), ("n", ctypes.c_uint32), ("max_headers", ctypes.c_uint32),
                 ("mode", ctypes.c_uint32), ("layout", ctypes.c_uint32), ("reqs", ctypes.c_void_p),
-                ("hdrs", ctypes.c_void_p), ("http", ctypes.c_void_p), ("work", ctypes.c_void_p)]
+                ("hdrs", ctypes.c_void_p), ("http", ctypes.c_void_p), ("work", ctypes.c_void_p),
+                ("last_len", ctypes.c_void_p)]
 
 
 # exported C-ABI symbols of librhp.so, as declared in include/rhp.h
@@ -202,21 +203,24 @@ def hdr_view(flat: np.ndarray, n: int, max_headers: int, layout: int) -> np.ndar
     return flat[: n * max_headers].reshape(n, max_headers)
 
 
-def _host_batch(buf, off, max_headers, mode, layout=LAYOUT_REQUEST_MAJOR):
+def _host_batch(buf, off, max_headers, mode, layout=LAYOUT_REQUEST_MAJOR, last_len=None):
     n = len(off) - 1
     reqs = np.zeros(n, dtype=REQ_DTYPE)
     hdrs = np.zeros(max(max_headers * n, 1), dtype=HDR_DTYPE)
     http = np.zeros(n, dtype=HTTP_DTYPE)
     rw = buf.copy()
     b = Batch(_ptr(rw), _ptr(rw), _ptr(off), rw.size, n, max_headers, mode, layout, _ptr(reqs), _ptr(hdrs),
-              _ptr(http), 0)
+              _ptr(http), 0, _ptr(last_len) if last_len is not None else None)
     return b, Result(reqs, hdr_view(hdrs, n, max_headers, layout), http if mode == MODE_HTTP else None, rw)
 
 
 def emulate(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,
-            layout: int = LAYOUT_REQUEST_MAJOR):
-    """Run the kernel's DFA algorithm on the CPU (tests).  Returns (Result, stats[3])."""
-    b, res = _host_batch(buf, off, max_headers, mode, layout)
+            layout: int = LAYOUT_REQUEST_MAJOR, last_len: np.ndarray | None = None):
+    """Run the kernel's DFA algorithm on the CPU (tests).  Returns (Result, stats[3]).
+    last_len: optional u64[n], phr_parse_request's last_len per request (phr mode)."""
+    if last_len is not None:
+        last_len = np.ascontiguousarray(last_len, dtype=np.uint64)
+    b, res = _host_batch(buf, off, max_headers, mode, layout, last_len)
     stats = np.zeros(3, dtype=np.uint64)
     rc = host().rhp_emu_parse_batch(ctypes.byref(b), _ptr(stats))
     if rc != 0:
@@ -236,7 +240,7 @@ class DeviceBatch:
     """A batch resident in HBM plus its output buffers (torch tensors as plumbing)."""
 
     def __init__(self, buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,
-                 device: str = "cuda", layout: int = LAYOUT_REQUEST_MAJOR):
+                 device: str = "cuda", layout: int = LAYOUT_REQUEST_MAJOR, last_len: np.ndarray | None = None):
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("no GPU visible: the rhp product path runs on MI355X only")
@@ -252,11 +256,14 @@ class DeviceBatch:
         self.http = torch.zeros((self.n if mode == MODE_HTTP else 1) * HTTP_DTYPE.itemsize, dtype=torch.uint8,
                                 device=device)
         self.work = torch.zeros(RHP_WORK_WORDS, dtype=torch.int32, device=device)
+        self.last_len = (torch.from_numpy(np.ascontiguousarray(last_len, dtype=np.uint64).view(np.int64)).to(device)
+                         if last_len is not None else None)
 
     def desc(self) -> Batch:
         return Batch(self.bytes.data_ptr(), self.bytes.data_ptr(), self.offsets.data_ptr(), self.bytes.numel(),
                      self.n, self.max_headers, self.mode, self.layout, self.reqs.data_ptr(), self.hdrs.data_ptr(),
-                     self.http.data_ptr(), self.work.data_ptr())
+                     self.http.data_ptr(), self.work.data_ptr(),
+                     self.last_len.data_ptr() if self.last_len is not None else None)
 
     def launch(self, stream=None) -> None:
         import torch
@@ -277,11 +284,11 @@ class DeviceBatch:
 
 
 def parse_batch(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,
-                impl: int = IMPL_DFA, layout: int = LAYOUT_REQUEST_MAJOR) -> Result:
+                impl: int = IMPL_DFA, layout: int = LAYOUT_REQUEST_MAJOR, last_len: np.ndarray | None = None) -> Result:
     """Parse a host batch on the GPU (copies in, one launch, copies out)."""
     lib().rhp_set_impl(impl)
     try:
-        db = DeviceBatch(buf, off, max_headers, mode, layout=layout)
+        db = DeviceBatch(buf, off, max_headers, mode, layout=layout, last_len=last_len)
         db.launch()
         return db.result()
     finally:

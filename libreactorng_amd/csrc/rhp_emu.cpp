@@ -39,7 +39,18 @@ void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
   const uint64_t hs_hdr = b->layout == RHP_LAYOUT_HEADER_MAJOR ? b->n : 1u;
   rhp_hdr_t *h = b->hdrs + i * hs_req;
   if (b->mode == RHP_MODE_HTTP) scalar_http(b->bytes_rw + off, len, b->max_headers, &r, h, hs_hdr, &b->http[i]);
-  else scalar_phr(b->bytes + off, len, b->max_headers, &r, h, hs_hdr);
+  else {
+    const uint64_t ll = b->last_len ? b->last_len[i] : 0;
+    const int pre = ll ? is_complete(b->bytes + off, len, ll) : 0;   /* picohttpparser.c:399-401 */
+    if (pre != 0) {
+      memset(&r, 0, sizeof r);
+      r.ret = pre;
+      r.minor_version = -1;
+      r.flags = RHP_F_EXACT;
+    } else {
+      scalar_phr(b->bytes + off, len, b->max_headers, &r, h, hs_hdr);
+    }
+  }
   b->reqs[i] = r;
 }
 
@@ -108,11 +119,15 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
       const bool ovf = d.ovf != 0;
       if (!(ovf || slow || term_ev || pos >= (int32_t) len)) continue;
       /* ---- finalize (same decisions as the kernel) ---- */
-      const bool ok = !ovf && is_done2(st) && term_pos < len && term_pos < RHP_MAX_LEN;
+      bool ok = !ovf && is_done2(st) && term_pos < len && term_pos < RHP_MAX_LEN;
       /* an ERR in the version (request line events ME, PE consumed) needs the
        * version's 9 bytes: len >= PE + 10 (picohttpparser.c:248-251) */
-      const bool bad = ovf ? d.ovf - 1u < len
-                           : (is_err2(st) && term_pos < len && (d.k != 2 || d.e[0] + 10u <= len));
+      bool bad = ovf ? d.ovf - 1u < len
+                     : (is_err2(st) && term_pos < len && (d.k != 2 || d.e[0] + 10u <= len));
+      if (b->mode == RHP_MODE_PHR && b->last_len && b->last_len[i] != 0) {   /* as the kernel's decode_end */
+        ok = ok && (b->last_len[i] < 3u || b->last_len[i] <= term_pos);
+        bad = false;
+      }
       if (ok) {
         st_count.fast_ok++;
         rhp_req_t r;

@@ -54,6 +54,7 @@ struct Params {
   rhp_req_t *reqs;
   rhp_hdr_t *hdrs;
   rhp_http_t *http;
+  const uint64_t *last_len;   /* phr mode, may be NULL: is_complete first where != 0 */
   uint32_t n;
   uint32_t max_headers;
   uint32_t mode;
@@ -178,7 +179,19 @@ __device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64
     p.http[i] = x;
   } else {
     LineBytes B{p.bytes + off, ~0ull, {0, 0, 0, 0}};
-    scalar_phr_t(B, len, p.max_headers, &r, h, p.hs_hdr);
+    const uint64_t ll = p.last_len ? p.last_len[i] : 0;
+    /* phr_parse_request runs is_complete first when last_len != 0
+     * (picohttpparser.c:399-401); its -2 / -1 is the answer */
+    const int pre = ll ? is_complete_t(B, len, ll) : 0;
+    if (pre != 0) {
+      r.ret = pre;
+      r.method_len = r.path_off = r.path_len = 0;
+      r.method_off = 0;
+      r.minor_version = -1;
+      r.num_headers = 0;
+    } else {
+      scalar_phr_t(B, len, p.max_headers, &r, h, p.hs_hdr);
+    }
   }
   p.reqs[i] = r;
 }
@@ -368,7 +381,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * need one), so the waves of a workgroup drain one shared range request by
    * request and finish together; no global atomic is ever touched.
    * Window addresses are u32 byte offsets from `base` (the 4-aligned start of
-   * the range; the host keeps a batch below 4 GiB). */
+   * the range; a range below 4 GiB is checked after the prologue loads). */
   const uint32_t wg_lo = min(blockIdx.x * p.span, p.n), wg_hi = min(wg_lo + p.span, p.n);
   /* the first WAVES * 64 requests of the range go to the threads in order
    * (first_n); refills hand out the rest from the LDS counter */
@@ -401,9 +414,20 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   }
   const uint64_t o_lo = pool_dry ? 0 : p.offsets[wg_lo], o_hi = pool_dry ? 0 : p.offsets[wg_hi];
   const uint64_t base = o_lo & ~(uint64_t) 3;
+  if (o_hi - base >= 0xFFFF0000ull) {
+    /* The window offsets below are u32 from `base`: a workgroup whose range
+     * spans ~4 GiB (a request of that size among its requests) parses its
+     * range with the exact path, one request per thread.  Every other range of
+     * the batch, wherever it lies, runs the DFA. */
+    for (uint32_t i = wg_lo + tid; i < wg_hi; i += WAVES * 64) {
+      const uint64_t off = p.offsets[i];
+      finish_exact(p, i, off, p.offsets[i + 1] - off);
+    }
+    return;
+  }
   const uint8_t *wbytes = p.bytes + base;
   /* the range's bytes as a raw buffer: window loads take 32-bit offsets from
-   * base (a batch is below 4 GiB), no 64-bit address per load */
+   * base (the range is below 4 GiB, checked above), no 64-bit address per load */
   const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(wbytes), 0, -1, 0x00020000);
 
   /* ---- walk state (the request whose window landed) ---- */
@@ -451,7 +475,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   /* give every lane without a pending request one from the pool; the offsets
    * loads are only consumed at the top of the next block */
   auto take = [&](uint32_t i) {
-    /* only the low dwords: a batch is below 4 GiB, so offsets relative to
+    /* only the low dwords: the range is below 4 GiB, so offsets relative to
      * `base` and lengths are exact modulo 2^32 */
     const uint32_t *o = reinterpret_cast<const uint32_t *>(p.offsets + i);
     pend = i;
@@ -780,12 +804,24 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const bool term_ev = is_done2(e) || is_err2(e);
     const bool fin = dhas && (ovfl || is_slow2(e) || term_ev || (uint32_t) dpos + kBlock >= dlen);
     if (!fin) return false;
-    const bool ok = !ovfl && is_done2(e) && term_pos < dlen && term_pos < RHP_MAX_LEN;
+    bool ok = !ovfl && is_done2(e) && term_pos < dlen && term_pos < RHP_MAX_LEN;
     /* an ERR between the path and the request-line end (the version, kn == 2)
      * is -1 only when the version's 9 bytes are there (picohttpparser.c:248-251):
      * len >= PE + 10 */
-    const bool bad = ovfl ? ovf - 1u < dlen
-                          : (is_err2(e) && term_pos < dlen && ((kn & 7u) != 2u || pe + 10u <= dlen));
+    bool bad = ovfl ? ovf - 1u < dlen
+                    : (is_err2(e) && term_pos < dlen && ((kn & 7u) != 2u || pe + 10u <= dlen));
+    if (!http && p.last_len) {
+      /* last_len != 0 (rare: a batch that carries it): is_complete runs first
+       * (picohttpparser.c:399-401).  Scanning from last_len - 3 at or before
+       * the first CR of the final CRLFCRLF of a request the DFA accepted, it
+       * meets only CRLF line ends and stops at that empty line: the parse
+       * stands.  Anything else (a later start, an ERR) takes the exact path. */
+      const uint64_t ll = p.last_len[dcur];
+      if (ll != 0) {
+        ok = ok && (ll < 3u || ll <= term_pos);
+        bad = false;
+      }
+    }
     /* the record as four dwords (rhp.h rhp_req_t: ret; method_len, path_off;
      * path_len, method_off 0, minor_version; num_headers, flags) */
     u32x4 rq = u32x4{0u, 0u, 0xff000000u, 0u};   /* minor_version -1 */
@@ -999,7 +1035,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * dispatched last in a workgroup run slowest and finish its range last.
    * Rotating every wave's priority each iteration (phase by wave) shares the
    * issue slots evenly (config 2 -1 %, configs 3 and 5 -3 %). */
-  uint32_t prio_it = (tid >> 6) & 3u;
+#ifndef RHP_PRIO_PHASE_SHIFT
+#define RHP_PRIO_PHASE_SHIFT 6
+#endif
+  uint32_t prio_it = (tid >> RHP_PRIO_PHASE_SHIFT) & 3u;
   while (!idle_wave) {
     prio_it = (prio_it + 1u) & 3u;
     switch (prio_it) {
@@ -1418,6 +1457,7 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   if (b->mode == RHP_MODE_HTTP && (!b->http || !b->bytes_rw)) return -22;
   if (b->mode != RHP_MODE_PHR && b->mode != RHP_MODE_HTTP) return -22;
   if (b->layout != RHP_LAYOUT_REQUEST_MAJOR && b->layout != RHP_LAYOUT_HEADER_MAJOR) return -22;
+  if (b->last_len && b->mode != RHP_MODE_PHR) return -22;   /* http_read_request passes last_len 0 */
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int dev = 0, cus = 0;
   {
@@ -1435,6 +1475,7 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.reqs = b->reqs;
   prm.hdrs = b->hdrs;
   prm.http = b->http;
+  prm.last_len = b->last_len;
   prm.n = b->n;
   prm.max_headers = b->max_headers;
   prm.mode = b->mode;
@@ -1443,9 +1484,9 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.hs_req = hmajor ? 1u : b->max_headers;
   prm.hs_hdr = hmajor ? b->n : 1u;
 
-  /* the DFA kernel addresses windows with u32 offsets from its range start;
-   * batches of 4 GiB or more take the exact kernel */
-  if (t_impl == RHP_IMPL_EXACT || b->bytes_size >= 0xFFFF0000ull) {
+  /* the DFA kernel addresses windows with u32 offsets from its workgroup's
+   * range start; a range of ~4 GiB runs the exact path inside it */
+  if (t_impl == RHP_IMPL_EXACT) {
     uint32_t grid = (b->n + 255) / 256;
     if (grid > (uint32_t) cus * 8) grid = (uint32_t) cus * 8;
     hipLaunchKernelGGL(rhp_exact_kernel, dim3(grid), dim3(256), 0, s, prm);

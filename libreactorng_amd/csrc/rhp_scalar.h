@@ -190,18 +190,20 @@ RHP_HD int scalar_phr(const uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r
 /* is_complete (picohttpparser.c:197-223), the slowloris pre-check that
  * phr_parse_request runs first when last_len != 0 (:399-401): 0 when an empty
  * line ends the bytes seen (scanning from last_len - 3), else -2 / -1. */
-RHP_HD int is_complete(const uint8_t *b, uint64_t len, uint64_t last_len)
+template <class Bytes>
+RHP_HD int is_complete_t(Bytes &B, uint64_t len, uint64_t last_len)
 {
   uint64_t p = last_len < 3 ? 0 : last_len - 3;
   int ret_cnt = 0;
   for (;;) {
-    if (p == len) return kPartial;
-    if (b[p] == '\r') {
+    if (p >= len) return kPartial;   /* CHECK_EOF; p > len only when last_len > len + 3 (off contract) */
+    const uint32_t c = B(p);
+    if (c == '\r') {
       ++p;
       if (p == len) return kPartial;
-      if (b[p++] != '\n') return kBad;
+      if (B(p++) != '\n') return kBad;
       ++ret_cnt;
-    } else if (b[p] == '\n') {
+    } else if (c == '\n') {
       ++p;
       ++ret_cnt;
     } else {
@@ -210,6 +212,12 @@ RHP_HD int is_complete(const uint8_t *b, uint64_t len, uint64_t last_len)
     }
     if (ret_cnt == 2) return 0;
   }
+}
+
+RHP_HD int is_complete(const uint8_t *b, uint64_t len, uint64_t last_len)
+{
+  PlainBytes B{b};
+  return is_complete_t(B, len, last_len);
 }
 
 /* ---- http_read_request framing (http.c:177-234) over a parsed request ---- */

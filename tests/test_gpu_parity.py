@@ -191,3 +191,55 @@ def test_gpu_version_errors(impl, shift):
         res = rhp.parse_batch(buf, off, 16, mode, impl=impl)
         want = to_rhp(*run_oracle(buf, off, 16, mode)[:3], mode)
         assert_same(canon(res, mode), want, buf, off, f"GPU version impl{impl} shift{shift} mode{mode}")
+
+
+@pytest.mark.parametrize("impl,layout", [(rhp.IMPL_DFA, rhp.LAYOUT_REQUEST_MAJOR), (rhp.IMPL_DFA, rhp.LAYOUT_HEADER_MAJOR),
+                                         (rhp.IMPL_DFA_LATE, rhp.LAYOUT_REQUEST_MAJOR),
+                                         (rhp.IMPL_EXACT, rhp.LAYOUT_REQUEST_MAJOR)])
+def test_gpu_last_len_matches_reference_golden(impl, layout):
+    """rhp_batch_t.last_len: is_complete first where last_len != 0
+    (picohttpparser.c:197-223, 399-401), against the reference's answers."""
+    top = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    buf, off = inputs(top["phr_last_len"])
+    z = np.load(os.path.join(GOLDEN, "phr_last_len.npz"))
+    res = rhp.parse_batch(buf, off, 16, rhp.MODE_PHR, impl=impl, layout=layout, last_len=z["last_len"])
+    assert_same(canon(res, rhp.MODE_PHR), (z["reqs"], z["hdrs"], None), buf, off, f"GPU impl{impl} last_len")
+
+
+def test_gpu_last_len_sweep_vs_emulation():
+    """Every last_len in 0 .. len + 3 on fuzz and config-2 requests: the GPU
+    equals the kernel emulation (itself pinned to the pointer parser on CPU)."""
+    from test_oracle_golden import last_len_sweep
+    buf, off, last = last_len_sweep()
+    want, _ = rhp.emulate(buf, off, 16, rhp.MODE_PHR, last_len=last)
+    for impl in (rhp.IMPL_DFA, rhp.IMPL_EXACT):
+        res = rhp.parse_batch(buf, off, 16, rhp.MODE_PHR, impl=impl, last_len=last)
+        assert_same(canon(res, rhp.MODE_PHR), canon(want, rhp.MODE_PHR), buf, off, f"GPU impl{impl} last_len sweep")
+
+
+@pytest.mark.parametrize("mode", [rhp.MODE_PHR, rhp.MODE_HTTP])
+def test_gpu_batch_over_4gib(mode):
+    """A batch larger than 4 GiB: a first request of 4 GiB + 4 KiB (its
+    workgroup's range cannot use the u32 window offsets and runs the exact path)
+    and 300k config-2 requests behind it, at absolute offsets above 4 GiB, on
+    the DFA path.  Expected records: the oracle on the same requests packed
+    without the giant one (a request's records depend only on its own bytes and
+    the bytes after it)."""
+    head = b"GET /big HTTP/1.1\r\nHost: x\r\n\r\n"
+    big = (1 << 32) + 4096 + 3
+    nb, no = rhp.generate(rhp.GEN_GET256, 300000, 4242)
+    nbytes = int(no[-1])
+    buf = np.zeros(big + nbytes + rhp.RHP_PAD, dtype=np.uint8)
+    buf[:len(head)] = np.frombuffer(head, dtype=np.uint8)
+    buf[big:big + nbytes] = nb[:nbytes]
+    off = np.concatenate([np.zeros(1, dtype=np.uint64), no.astype(np.uint64) + np.uint64(big)])
+    res = rhp.parse_batch(buf, off, 16, mode)
+    got = canon(res, mode)
+    want = to_rhp(*run_oracle(nb, no, 16, mode)[:3], mode)
+    assert_same(tuple(x[1:] if x is not None else None for x in got), want, nb, no, "over 4 GiB: the requests after")
+    sbuf, soff = pack([head + bytes(64)])
+    w0 = to_rhp(*run_oracle(sbuf, soff, 16, mode)[:3], mode)
+    assert got[0][0] == w0[0][0] and (got[1][0] == w0[1][0]).all()
+    if mode == rhp.MODE_HTTP:
+        assert got[2][0] == w0[2][0]
+    del res, buf

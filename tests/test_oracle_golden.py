@@ -138,3 +138,48 @@ def test_diff_fuzz_oracle_vs_compiled_reference():
     out = subprocess.run([os.path.join(root, "oracle", "_ref", "diff_fuzz"), "42", "2000", "7"], capture_output=True,
                          text=True, timeout=300)
     assert out.returncode == 0 and "diff_fuzz OK: 84000 requests" in out.stdout, out.stdout + out.stderr
+
+
+@pytest.mark.parametrize("layout", [rhp.LAYOUT_REQUEST_MAJOR, rhp.LAYOUT_HEADER_MAJOR])
+def test_batch_last_len_emulation_matches_reference_golden(layout):
+    """rhp_batch_t.last_len (phr mode): the kernel's decisions (rhp_emu.cpp) with
+    is_complete first where last_len != 0 (picohttpparser.c:197-223, 399-401),
+    against the compiled reference's answers (tests/golden/phr_last_len.npz)."""
+    spec = MANIFEST["phr_last_len"]
+    buf, off = inputs(spec)
+    z = np.load(os.path.join(GOLDEN, "phr_last_len.npz"))
+    res, stats = rhp.emulate(buf, off, 16, rhp.MODE_PHR, layout, last_len=z["last_len"])
+    assert_same(canon(res, rhp.MODE_PHR), (z["reqs"], z["hdrs"], None), buf, off, "emulation, last_len")
+    assert stats[0] > 0   # the DFA path still answers the requests is_complete cannot change
+
+
+def last_len_sweep():
+    """Each request of a mixed set repeated with last_len = 0 .. len + 3 (the
+    contract's range), in one batch."""
+    b1, o1 = rhp.generate(rhp.GEN_FUZZ, 120, 77)
+    b2, o2 = rhp.generate(rhp.GEN_GET256, 4, 78)
+    reqs = [bytes(b1[o1[i]:o1[i + 1]]) for i in range(len(o1) - 1)]
+    reqs += [bytes(b2[o2[i]:o2[i + 1]]) for i in range(len(o2) - 1)]
+    rep, last = [], []
+    for r in reqs:
+        for ll in sorted(set(list(range(0, min(len(r), 12) + 4)) + list(range(max(0, len(r) - 8), len(r) + 4)))):
+            rep.append(r)
+            last.append(ll)
+    from batches import pack
+    buf, off = pack(rep)
+    return buf, off, np.array(last, dtype=np.uint64)
+
+
+def test_batch_last_len_sweep_emulation_vs_pointer_parser():
+    buf, off, last = last_len_sweep()
+    res, _ = rhp.emulate(buf, off, 16, rhp.MODE_PHR, last_len=last)
+    for i in range(len(off) - 1):
+        ret, minor, m, p, hs = rhp.phr_parse_request_cpu(buf, int(off[i]), int(off[i + 1] - off[i]), 16, int(last[i]))
+        r = res.reqs[i]
+        assert r["ret"] == ret, (i, int(last[i]), r, ret)
+        if ret > 0:
+            assert (r["minor_version"], (r["method_off"], r["method_len"]), (r["path_off"], r["path_len"])) == \
+                (minor, m, p), i
+            got = [(-1 if h["name_off"] == rhp.RHP_NAME_NULL else int(h["name_off"]), int(h["name_len"]),
+                    int(h["value_off"]), int(h["value_len"])) for h in res.hdrs[i][: int(r["num_headers"])]]
+            assert got == hs, i

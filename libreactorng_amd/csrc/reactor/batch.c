@@ -61,6 +61,7 @@ typedef struct batch_state
 {
   int          parser;
   hipStream_t  stream;
+  hipStream_t  wstream;      /* the gpu writer's own stream: its syncs never wait for a queued parse round */
   int          efd;          /* gpu: written once per completed round */
   slot_t       slot[REACTOR_BATCH_SLOTS];
   void        *d_work;
@@ -97,13 +98,17 @@ static void *host_worker(void *arg)
     const int k = b->q[b->q_head];
     pthread_mutex_unlock(&b->mu);
     host_parse(b, k);
-    const uint64_t one = 1;
-    ssize_t r = write(b->efd, &one, sizeof one);
-    (void) r;
+    /* the entry leaves the queue before the loop thread hears of the round:
+     * it may finish the slot and submit it again right after the write */
     pthread_mutex_lock(&b->mu);
     b->q_head = (b->q_head + 1) % REACTOR_BATCH_SLOTS;
     b->q_n--;
     pthread_cond_broadcast(&b->cv);
+    pthread_mutex_unlock(&b->mu);
+    const uint64_t one = 1;
+    ssize_t r = write(b->efd, &one, sizeof one);
+    (void) r;
+    pthread_mutex_lock(&b->mu);
   }
   return NULL;
 }
@@ -304,6 +309,8 @@ void reactor_batch_submit(int k, uint32_t n, size_t bytes)
   if (B.parser == PARSER_HOST_ASYNC)
   {
     pthread_mutex_lock(&B.mu);
+    if (B.q_n >= REACTOR_BATCH_SLOTS)
+      die("reactor_batch_submit: queue full", B.q_n);
     B.q[(B.q_head + B.q_n) % REACTOR_BATCH_SLOTS] = k;
     B.q_n++;
     pthread_cond_broadcast(&B.cv);
@@ -396,10 +403,12 @@ int reactor_batch_writer(void)
                                                                                                         : WRITER_HOST);
     if (B.writer == 1 + WRITER_GPU && B.parser != PARSER_GPU)
     {
-      /* the gpu writer shares the gpu parser's stream */
+      /* the gpu writer runs on the gpu parser's device */
       fprintf(stderr, "reactor: RHP_REACTOR_WRITER=gpu needs RHP_REACTOR_PARSER=gpu\n");
       abort();
     }
+    if (B.writer == 1 + WRITER_GPU)
+      HIP(hipStreamCreateWithFlags(&B.wstream, hipStreamNonBlocking));
   }
   return B.writer - 1 != WRITER_HOST;
 }
@@ -457,7 +466,9 @@ void reactor_batch_write(const uint8_t *arena, size_t arena_n, const rhp_resp_t 
     (void) n_fields;
     return;
   }
-  /* gpu: H2D of the round's replies, rhp_write_responses, D2H (synchronous) */
+  /* gpu: H2D of the round's replies, rhp_write_responses, D2H (synchronous, on
+   * the writer's own stream: the next parse round, already queued on
+   * B.wstream, keeps running meanwhile) */
   grow_dev(&B.dw_arena, &B.w_cap_arena, arena_n + 16);
   size_t cap_n = B.w_cap_n;
   grow_dev(&B.dw_resps, &B.w_cap_n, (size_t) n * sizeof *resps + 16);
@@ -473,20 +484,20 @@ void reactor_batch_write(const uint8_t *arena, size_t arena_n, const rhp_resp_t 
     HIP(hipHostMalloc((void **) &B.hw_off, rn * sizeof(uint64_t), hipHostMallocDefault));
   }
   grow_dev(&B.dw_fields, &B.w_cap_f, (size_t) n_fields * sizeof *fields + 16);
-  HIP(hipMemcpyAsync(B.dw_arena, arena, arena_n, hipMemcpyHostToDevice, B.stream));
-  HIP(hipMemcpyAsync(B.dw_resps, resps, (size_t) n * sizeof *resps, hipMemcpyHostToDevice, B.stream));
+  HIP(hipMemcpyAsync(B.dw_arena, arena, arena_n, hipMemcpyHostToDevice, B.wstream));
+  HIP(hipMemcpyAsync(B.dw_resps, resps, (size_t) n * sizeof *resps, hipMemcpyHostToDevice, B.wstream));
   if (n_fields)
-    HIP(hipMemcpyAsync(B.dw_fields, fields, (size_t) n_fields * sizeof *fields, hipMemcpyHostToDevice, B.stream));
+    HIP(hipMemcpyAsync(B.dw_fields, fields, (size_t) n_fields * sizeof *fields, hipMemcpyHostToDevice, B.wstream));
   for (int pass = 0; pass < 2; pass++)
   {
     rhp_resp_batch_t w = {.arena = B.dw_arena, .resps = B.dw_resps, .fields = n_fields ? B.dw_fields : NULL, .n = n,
                           .date_len = RHP_DATE_LEN, .date = date, .out_off = B.dw_off, .out = B.dw_out,
                           .out_size = B.w_cap_out, .work = B.dw_work};
-    int rc = rhp_write_responses(&w, B.stream);
+    int rc = rhp_write_responses(&w, B.wstream);
     if (rc != 0)
       die("rhp_write_responses", rc);
-    HIP(hipMemcpyAsync(B.hw_off, B.dw_off, ((size_t) n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, B.stream));
-    HIP(hipStreamSynchronize(B.stream));
+    HIP(hipMemcpyAsync(B.hw_off, B.dw_off, ((size_t) n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, B.wstream));
+    HIP(hipStreamSynchronize(B.wstream));
     if (B.hw_off[n] <= B.w_cap_out)
       break;
     /* the output did not fit: grow it and write again (rhp.h) */
@@ -500,8 +511,8 @@ void reactor_batch_write(const uint8_t *arena, size_t arena_n, const rhp_resp_t 
     HIP(hipHostMalloc((void **) &B.hw_out, c, hipHostMallocDefault));
     B.w_cap_out = c;
   }
-  HIP(hipMemcpyAsync(B.hw_out, B.dw_out, B.hw_off[n], hipMemcpyDeviceToHost, B.stream));
-  HIP(hipStreamSynchronize(B.stream));
+  HIP(hipMemcpyAsync(B.hw_out, B.dw_out, B.hw_off[n], hipMemcpyDeviceToHost, B.wstream));
+  HIP(hipStreamSynchronize(B.wstream));
   *out = B.hw_out;
   *out_off = B.hw_off;
 }

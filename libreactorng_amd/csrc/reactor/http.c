@@ -42,7 +42,7 @@ void reactor_http_fill(const uint8_t *base, const rhp_req_t *r, const rhp_hdr_t 
   *target = data(base + r->path_off, r->path_len);
   for (uint32_t k = 0; k < r->num_headers; k++)
   {
-    const rhp_hdr_t *o = &h[k * hs];   /* header-major batch records (rhp.h) */
+    const rhp_hdr_t *o = &h[k * hs];   /* record k at h[k * hs] (hs = 1 request-major, n header-major; rhp.h) */
     fields[k].name = o->name_off == RHP_NAME_NULL ? data_null() : data(base + o->name_off, o->name_len);
     fields[k].value = data(base + o->value_off, o->value_len);
   }

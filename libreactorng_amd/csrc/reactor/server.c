@@ -187,12 +187,15 @@ typedef struct round
   size_t             n_pieces, cap_pieces;
 } round_t;
 
-/* the rounds in flight on this thread, in submission order (slot = index) */
+/* the rounds in flight on this thread, in submission order (slot = index);
+ * the slots are shared by every server of the thread */
 static __thread struct
 {
-  round_t   r[REACTOR_BATCH_SLOTS];
-  int       head, count;
-  reactor_t poll;   /* the batch eventfd, registered while count > 0 */
+  round_t    r[REACTOR_BATCH_SLOTS];
+  int        head, count;
+  reactor_t  poll;       /* the batch eventfd, registered while count > 0 */
+  server_t **waiting;    /* servers turned away while every slot was in flight */
+  size_t     n_waiting, cap_waiting;
 } R;
 
 
@@ -471,6 +474,35 @@ static void round_finish(round_t *r, int k, bool dispatch)
     rs_dispatch_ns += rs_now() - t0;
 }
 
+/* A server whose batch round found every slot in flight waits here; the next
+ * completion re-arms every waiting server (not only the one whose round
+ * completed: the slots are shared by all servers of the thread) */
+static void server_wait_slot(server_t *server)
+{
+  for (size_t i = 0; i < R.n_waiting; i++)
+    if (R.waiting[i] == server)
+      return;
+  R.waiting = grow(R.waiting, &R.cap_waiting, R.n_waiting + 1, sizeof *R.waiting);
+  R.waiting[R.n_waiting++] = server;
+}
+
+static void server_wait_remove(server_t *server)
+{
+  for (size_t i = 0; i < R.n_waiting; i++)
+    if (R.waiting[i] == server)
+      R.waiting[i--] = R.waiting[--R.n_waiting];
+}
+
+static void server_wake_waiting(void)
+{
+  while (R.n_waiting)
+  {
+    server_t *server = R.waiting[--R.n_waiting];
+    if (!list_is_empty(&server->queue) && !server->batch)
+      server->batch = reactor_next(server_batch_run, server);
+  }
+}
+
 static void server_batch_ready(reactor_event_t *event)
 {
   (void) event;
@@ -481,6 +513,8 @@ static void server_batch_ready(reactor_event_t *event)
     R.count--;
     round_finish(&R.r[k], k, true);
   }
+  if (R.count < REACTOR_BATCH_SLOTS)
+    server_wake_waiting();
   if (!R.count && R.poll)
   {
     reactor_poll_remove(R.poll);
@@ -494,7 +528,10 @@ static void server_batch_run(reactor_event_t *event)
   server->batch = 0;
   round_stats_init();
   if (R.count == REACTOR_BATCH_SLOTS)
-    return;   /* every slot in flight: the next completion schedules this again */
+  {
+    server_wait_slot(server);   /* every slot in flight: the next completion schedules this again */
+    return;
+  }
   const uint64_t t0 = round_stats ? rs_now() : 0;
   const int k = (R.head + R.count) % REACTOR_BATCH_SLOTS;
   round_t *r = &R.r[k];
@@ -552,6 +589,7 @@ static void server_rounds_drain(server_t *server)
     reactor_poll_remove(R.poll);
     R.poll = 0;
   }
+  server_wake_waiting();   /* other servers of the thread that waited for a slot */
 }
 
 /* -------------------------------------------------------------- public */
@@ -568,6 +606,7 @@ void server_destruct(server_t *server)
 {
   server_close(server);
   timeout_destruct(&server->timeout);
+  server_wait_remove(server);
   server_rounds_drain(server);
   while (!list_is_empty(&server->sessions))
   {

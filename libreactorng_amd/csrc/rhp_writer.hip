@@ -28,6 +28,7 @@
  * Byte copies are HBM-bound; the response bytes written are the algorithmic bytes.
  */
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <stdint.h>
 #include <string.h>
 
@@ -326,7 +327,9 @@ __global__ __launch_bounds__(256) void rhp_resp_write_kernel(WParams p)
   }
 }
 
-int g_writer_cus = 0;
+/* the CU count per device id (one host thread per GPU may call concurrently) */
+constexpr int kWriterMaxDevices = 64;
+std::atomic<int> g_writer_cus[kWriterMaxDevices];
 
 }  // namespace
 
@@ -338,11 +341,17 @@ extern "C" int rhp_write_responses(const rhp_resp_batch_t *b, void *stream)
   if (!b->out && b->out_size != 0) return -22;
   if (b->n > 0 && !b->work) return -22;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (g_writer_cus == 0) {
-    int dev = 0;
+  int dev = 0, cus = 0;
+  {
     hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&g_writer_cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return (int) e;
+    if (dev < 0 || dev >= kWriterMaxDevices) return -22;
+    cus = g_writer_cus[dev].load(std::memory_order_relaxed);
+    if (cus == 0) {
+      e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (e != hipSuccess) return (int) e;
+      g_writer_cus[dev].store(cus, std::memory_order_relaxed);
+    }
   }
   WParams p;
   p.arena = b->arena;
@@ -355,7 +364,7 @@ extern "C" int rhp_write_responses(const rhp_resp_batch_t *b, void *stream)
   memset(p.date, 0, sizeof p.date);
   memcpy(p.date, b->date, RHP_DATE_LEN);
   if (b->n == 0) return (int) hipMemsetAsync(b->out_off, 0, sizeof(uint64_t), s);
-  const uint32_t cap = (uint32_t) g_writer_cus * 8u;
+  const uint32_t cap = (uint32_t) cus * 8u;
   const uint32_t tiles = (b->n + kTile - 1u) / kTile;
   hipLaunchKernelGGL(rhp_resp_tile_sum_kernel, dim3(tiles), dim3(1024), 0, s, p, b->work);
   hipLaunchKernelGGL(rhp_resp_top_scan_kernel, dim3(1), dim3(1024), 0, s, b->work, tiles);

@@ -26,7 +26,7 @@
 
 #include "reactor.h"
 
-static int port;
+static int port, port2;
 static int stop_pipe[2];
 static atomic_long calls;
 static int failures;
@@ -79,19 +79,20 @@ static void server_callback(reactor_event_t *event)
     server_plain(session, string("ok"), NULL, 0);
 }
 
-static server_t server;
+static server_t server, server2;   /* two servers on one reactor thread share its batch slots */
 
 static void stop_ready(reactor_event_t *event)
 {
   reactor_poll_remove(*(reactor_t *) event->state);
   server_destruct(&server);
+  server_destruct(&server2);
 }
 
 /* ---------------------------------------------------------------- client */
 
-static int client(void)
+static int client_port(int p)
 {
-  struct sockaddr_in sin = {.sin_family = AF_INET, .sin_addr.s_addr = htonl(0x7f000001), .sin_port = htons(port)};
+  struct sockaddr_in sin = {.sin_family = AF_INET, .sin_addr.s_addr = htonl(0x7f000001), .sin_port = htons(p)};
   int c = socket(AF_INET, SOCK_STREAM, 0);
   struct timeval tv = {.tv_sec = 10};
   (void) setsockopt(c, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
@@ -104,6 +105,8 @@ static int client(void)
   }
   return c;
 }
+
+static int client(void) { return client_port(port); }
 
 static void send_all(int c, const char *p, size_t n)
 {
@@ -270,6 +273,7 @@ static const char tfb[] = "GET /plaintext HTTP/1.1\r\nHost: tfb-server:8080\r\nA
 typedef struct load_arg
 {
   int   requests;
+  int   port;
   long  got;
 } load_arg_t;
 
@@ -278,7 +282,7 @@ static void *load_client(void *p)
   load_arg_t *a = p;
   static __thread reader_t r;
   char body[64];
-  int c = client();
+  int c = client_port(a->port);
   if (c < 0)
     return NULL;
   r.len = 0;
@@ -325,7 +329,10 @@ static void *client_main(void *unused)
            1, "hello world", 0);
   run_case("lf line ends x2", "GET / HTTP/1.1\n\nGET / HTTP/1.1\n\n", 2, "ok", 0);
   long_cases();
-  /* load: many connections, pipelined */
+  /* load: many connections, pipelined, on both servers at once (a server
+   * turned away while the other's rounds hold every batch slot must be
+   * re-armed by the next completion: ADVICE r2) */
+  for (int phase = 0; phase < 2; phase++)
   {
     pthread_t t[256];
     load_arg_t a[256];
@@ -334,7 +341,7 @@ static void *client_main(void *unused)
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int i = 0; i < n; i++)
     {
-      a[i] = (load_arg_t) {.requests = per_conn};
+      a[i] = (load_arg_t) {.requests = per_conn, .port = phase && (i & 1) ? port2 : port};
       pthread_create(&t[i], NULL, load_client, &a[i]);
     }
     long total = 0;
@@ -346,8 +353,8 @@ static void *client_main(void *unused)
     clock_gettime(CLOCK_MONOTONIC, &t1);
     double s = (double) (t1.tv_sec - t0.tv_sec) + (double) (t1.tv_nsec - t0.tv_nsec) * 1e-9;
     CHECK(total == (long) n * per_conn, "load: %ld responses, want %ld", total, (long) n * per_conn);
-    printf("load %d connections x %d pipelined: %ld responses in %.3f s (%.0f req/s)\n", n, per_conn, total, s,
-           (double) total / s);
+    printf("load %d connections x %d pipelined%s: %ld responses in %.3f s (%.0f req/s)\n", n, per_conn,
+           phase ? " (two servers)" : "", total, s, (double) total / s);
   }
   if (write(stop_pipe[1], "x", 1) != 1)
     abort();
@@ -368,12 +375,22 @@ int main(int argc, char **argv)
       getsockname(s, (struct sockaddr *) &sin, &len) != 0)
     return 2;
   port = ntohs(sin.sin_port);
+  struct sockaddr_in sin2 = {.sin_family = AF_INET, .sin_addr.s_addr = htonl(0x7f000001)};
+  int s2 = socket(AF_INET, SOCK_STREAM, 0);
+  (void) setsockopt(s2, SOL_SOCKET, SO_REUSEADDR, (int[]) {1}, sizeof(int));
+  len = sizeof sin2;
+  if (bind(s2, (struct sockaddr *) &sin2, sizeof sin2) != 0 || listen(s2, 4096) != 0 ||
+      getsockname(s2, (struct sockaddr *) &sin2, &len) != 0)
+    return 2;
+  port2 = ntohs(sin2.sin_port);
   if (pipe(stop_pipe) != 0)
     return 2;
 
   reactor_construct();
   server_construct(&server, server_callback, NULL);
   server_open_socket(&server, s);
+  server_construct(&server2, server_callback, NULL);
+  server_open_socket(&server2, s2);
   reactor_t stop = reactor_poll(stop_ready, &stop, stop_pipe[0], EPOLLIN);
   printf("parser: %s\n", reactor_parser_name());
   pthread_t t;
@@ -382,6 +399,7 @@ int main(int argc, char **argv)
   pthread_join(t, NULL);
   reactor_destruct();
   close(s);
+  close(s2);
   printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);
   return failures != 0;
 }

@@ -205,14 +205,18 @@ class GpuRunner:
     """A config's shard resident in HBM (rotated copies), launched on torch's
     current stream and timed with HIP events on that stream."""
 
-    def __init__(self, cfg, lo, hi, copies, layout):
+    def __init__(self, cfg, lo, hi, copies, layout, streams=1):
         import torch
         self.torch = torch
         buf, off = rhp.generate(cfg["gen"], hi - lo, cfg["seed"], lo=lo)
         self.copies = [rhp.DeviceBatch(buf, off, cfg["maxh"], cfg["mode"], layout=layout) for _ in range(max(1, copies))]
-        for c in self.copies[1:]:   # one set of output records
-            c.reqs, c.hdrs, c.http = self.copies[0].reqs, self.copies[0].hdrs, self.copies[0].http
+        # one set of output records per stream (batches in flight at once never share outputs)
+        self.nstreams = max(1, streams)
+        for k, c in enumerate(self.copies):
+            o = self.copies[k % self.nstreams]
+            c.reqs, c.hdrs, c.http = o.reqs, o.hdrs, o.http
         self.stream = torch.cuda.current_stream()
+        self.streams = [self.stream] + [torch.cuda.Stream() for _ in range(self.nstreams - 1)]
 
     def step(self, k):
         self.copies[k % len(self.copies)].launch(self.stream)
@@ -242,6 +246,27 @@ class GpuRunner:
             print(f"bench diag: record {1e3 * (t1 - t0):.3f} ms, {steps} launches {1e3 * (t2 - t1):.3f} ms, "
                   f"record+sync {1e3 * (t3 - t2):.3f} ms", file=sys.stderr)
         return t3 - t0, ev0.elapsed_time(ev1) / steps
+
+    def timed_pipelined(self, steps):
+        """Wall seconds for `steps` launches, launch k on stream k % S: batch k+1
+        starts on the CUs batch k's tail has freed (two batches in flight, as
+        the reactor's two batch slots)."""
+        torch = self.torch
+        start, ends = torch.cuda.Event(), [torch.cuda.Event() for _ in self.streams]
+        torch.cuda.synchronize()
+        gc.collect()
+        t0 = time.perf_counter()
+        start.record(self.stream)
+        for s in self.streams[1:]:
+            s.wait_event(start)
+        for k in range(steps):
+            self.copies[k % len(self.copies)].launch(self.streams[k % self.nstreams])
+        for e, s in zip(ends, self.streams):
+            e.record(s)
+        for e in ends:
+            self.stream.wait_event(e)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
 
     def ok_fraction(self):
         res = self.copies[0].result()

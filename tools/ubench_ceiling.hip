@@ -96,6 +96,84 @@ __global__ void chunk(const uint8_t *buf, uint8_t *reqs, uint8_t *hdrs, uint32_t
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
+
+/* wave per 64 requests: 16 loads of 1 KiB (U in flight), then the 64 records
+ * written coalesced: reqs 1 KiB (16 B per lane), each header k one 512-B run */
+template <int U, int NT, int W>
+__global__ void group(const uint8_t *buf, uint8_t *reqs, uint8_t *hdrs, uint32_t *out)
+{
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t waves = (uint64_t) gridDim.x * (blockDim.x >> 6);
+  uint32_t acc = 0;
+  for (uint64_t g = (uint64_t) blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); g < kReqs / 64; g += waves) {
+    const uint8_t *b = buf + g * 16384 + 16 * lane;
+    for (int j = 0; j < 16; j += U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        gq *p = (gq *) (uintptr_t) (b + 1024 * (j + u));
+        v[u] = NT ? __builtin_nontemporal_load(p) : *p;
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+    }
+    if (W) write_records(reqs, hdrs, g * 64 + lane, acc);
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
+/* group with the records written in other forms: WM 1 = nt stores (ABI layout),
+ * 2 = the wave's 3 KiB of records contiguous (tiled: reqs then the 4 header
+ * runs of its 64 requests), 3 = reqs only (16 MB), 4 = headers only (32 MB) */
+template <int U, int WM>
+__global__ void groupw(const uint8_t *buf, uint8_t *reqs, uint8_t *hdrs, uint32_t *out)
+{
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t waves = (uint64_t) gridDim.x * (blockDim.x >> 6);
+  uint32_t acc = 0;
+  typedef __attribute__((address_space(1))) u32x4 gw4;
+  typedef __attribute__((address_space(1))) u32x2 gw2;
+  for (uint64_t g = (uint64_t) blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); g < kReqs / 64; g += waves) {
+    const uint8_t *b = buf + g * 16384 + 16 * lane;
+    for (int j = 0; j < 16; j += U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load((gq *) (uintptr_t) (b + 1024 * (j + u)));
+#pragma unroll
+      for (int u = 0; u < U; u++) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+    }
+    const uint64_t i = g * 64 + lane;
+    if (WM == 1) {
+      __builtin_nontemporal_store(u32x4{acc, 1, 2, 3}, (gw4 *) (uintptr_t) (reqs + 16 * i));
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        __builtin_nontemporal_store(u32x2{acc, (uint32_t) k}, (gw2 *) (uintptr_t) (hdrs + 8 * ((uint64_t) k * kReqs + i)));
+    } else if (WM == 2) {
+      uint8_t *t = reqs + g * 3072;   /* reqs (16 MB) + hdrs (32 MB): one 48 MB area */
+      *(gw4 *) (uintptr_t) (t + 16 * lane) = u32x4{acc, 1, 2, 3};
+#pragma unroll
+      for (int k = 0; k < 4; k++) *(gw2 *) (uintptr_t) (t + 1024 + 512 * k + 8 * lane) = u32x2{acc, (uint32_t) k};
+    } else if (WM == 3) {
+      *(gw4 *) (uintptr_t) (reqs + 16 * i) = u32x4{acc, 1, 2, 3};
+    } else if (WM == 4) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) *(gw2 *) (uintptr_t) (hdrs + 8 * ((uint64_t) k * kReqs + i)) = u32x2{acc, (uint32_t) k};
+    }
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
+/* writes only: 48 MB with 16 B per lane, contiguous */
+__global__ void wonly(const uint8_t *, uint8_t *reqs, uint8_t *hdrs, uint32_t *out)
+{
+  typedef __attribute__((address_space(1))) u32x4 gw4;
+  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x * 16;
+  for (uint64_t at = ((uint64_t) blockIdx.x * blockDim.x + threadIdx.x) * 16; at < 48 * kReqs; at += stride) {
+    uint8_t *t = reqs + at;
+    *(gw4 *) (uintptr_t) t = u32x4{(uint32_t) at, 1, 2, 3};
+  }
+}
+
 struct Bufs {
   uint8_t *in[4];
   uint8_t *reqs, *hdrs;
@@ -135,8 +213,9 @@ int main()
     CHECK(hipMalloc(&b.in[k], kBytes + 4096));
     CHECK(hipMemset(b.in[k], k + 1, kBytes + 4096));
   }
-  CHECK(hipMalloc(&b.reqs, 16 * kReqs));
-  CHECK(hipMalloc(&b.hdrs, 32 * kReqs));
+  /* one area: reqs (16 MB) then hdrs (32 MB), plus slack */
+  CHECK(hipMalloc(&b.reqs, 48 * kReqs + 65536));
+  b.hdrs = b.reqs + 16 * kReqs;
   CHECK(hipMalloc(&b.out, 4 << 20));
   CHECK(hipMalloc(&b.ctr, 4 * 64 * 64));
   int cus = 0;
@@ -148,6 +227,24 @@ int main()
 #define CHUNK(U, NT, W, C, GRID, BLOCK)                                                                            \
   run("chunk" #C " U" #U " nt" #NT " w" #W " grid " #GRID "x" #BLOCK,                                            \
       [&](uint8_t *in, uint32_t *ctr) { hipLaunchKernelGGL((chunk<U, NT, W, C>), dim3(GRID), dim3(BLOCK), 0, 0, in, b.reqs, b.hdrs, b.out, ctr); }, b, true)
+#define GROUP(U, NT, W, GRID, BLOCK)                                                                              \
+  run("group U" #U " nt" #NT " w" #W " grid " #GRID "x" #BLOCK,                                                 \
+      [&](uint8_t *in, uint32_t *) { hipLaunchKernelGGL((group<U, NT, W>), dim3(GRID), dim3(BLOCK), 0, 0, in, b.reqs, b.hdrs, b.out); }, b, false)
+#define GROUPW(U, WM, GRID, BLOCK)                                                                              \
+  run("groupw U" #U " wm" #WM " grid " #GRID "x" #BLOCK,                                                        \
+      [&](uint8_t *in, uint32_t *) { hipLaunchKernelGGL((groupw<U, WM>), dim3(GRID), dim3(BLOCK), 0, 0, in, b.reqs, b.hdrs, b.out); }, b, false)
+  if (getenv("ONLY_W")) {
+    for (int rep = 0; rep < 2; rep++) {
+      GROUP(8, 1, 0, 256, 1024);
+      GROUP(8, 1, 1, 256, 1024);
+      GROUPW(8, 1, 256, 1024);
+      GROUPW(8, 2, 256, 1024);
+      GROUPW(8, 3, 256, 1024);
+      GROUPW(8, 4, 256, 1024);
+      run("wonly 48 MB", [&](uint8_t *in, uint32_t *) { hipLaunchKernelGGL(wonly, dim3(256 * 4), dim3(256), 0, 0, in, b.reqs, b.hdrs, b.out); }, b, false);
+    }
+    return 0;
+  }
   for (int rep = 0; rep < 2; rep++) {
     COAL(4, 1, 0, 256 * 4, 256);
     COAL(4, 1, 0, 256, 1024);
@@ -157,10 +254,13 @@ int main()
     COAL(4, 1, 1, 256, 1024);
     COAL(4, 1, 1, 256 * 4, 256);
     CHUNK(4, 1, 0, 65536, 256, 1024);
-    CHUNK(4, 1, 0, 16384, 256, 1024);
-    CHUNK(4, 1, 0, 16384, 512, 512);
     CHUNK(4, 1, 1, 65536, 256, 1024);
-    CHUNK(4, 1, 1, 16384, 512, 512);
+    GROUP(4, 1, 0, 256, 1024);
+    GROUP(8, 1, 0, 256, 1024);
+    GROUP(4, 1, 1, 256, 1024);
+    GROUP(8, 1, 1, 256, 1024);
+    GROUP(16, 1, 1, 256, 1024);
+    GROUP(8, 1, 1, 512, 512);
   }
   return 0;
 }

@@ -108,11 +108,9 @@ typedef struct rhp_batch {
   rhp_hdr_t      *hdrs;        /* device [n * max_headers] records, laid out as `layout` says
                                   (n * max_headers < 2^32) */
   rhp_http_t     *http;        /* device [n], RHP_MODE_HTTP */
-  uint32_t       *work;        /* device scratch of RHP_WORK_WORDS u32, zeroed before its first
-                                  use (the kernel leaves it zeroed), one launch at a time; or
-                                  NULL.  With it (and a batch below 4 GiB) workgroups that finish
-                                  their own range early take pieces of the others' ranges;
-                                  without it every range is parsed by its owner alone */
+  uint32_t       *work;        /* reserved, may be NULL (device scratch of RHP_WORK_WORDS u32
+                                  for future kernels; the current ones keep their scheduling
+                                  state in LDS) */
   const uint64_t *last_len;    /* device [n] or NULL (= all 0), RHP_MODE_PHR only:
                                   phr_parse_request's last_len per request
                                   (picohttpparser.c:383, 399-401): when last_len[i] != 0 the

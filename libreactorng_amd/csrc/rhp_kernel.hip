@@ -59,11 +59,6 @@ struct Params {
   uint32_t max_headers;
   uint32_t mode;
   uint32_t span;    /* requests per workgroup */
-  uint32_t *work;   /* cross-workgroup balancing (rhp.h `work`): [0] tail-piece counter,
-                       [1] workgroups done; NULL: every range is parsed by its owner */
-  uint32_t tail;    /* requests at the end of every even range that other workgroups may
-                       take (0: no balancing) */
-  uint32_t tail_pieces;   /* pieces of kPiece requests per tail */
   uint32_t hs_req;  /* record stride between requests (rhp_layout) */
   uint32_t hs_hdr;  /* ... between the records of one request */
 };
@@ -101,13 +96,10 @@ enum : uint32_t {
   kPoolWords = 8,                                /* counter, replay flag, long-list length, long-list
                                                     cursor, slow-list length, defer-list length */
   kOrderSpan = 8192,
-  kListCap = 1280,
-  kDeferCap = 240,                               /* the replay's list (defer): request indices */
-  kSlots = 32,                                   /* tail pieces one workgroup may take */
-  kPiece = 256,                                  /* requests per tail piece */
-  kPoolBytes = 4 * kPoolWords + kOrderSpan / 8 + 2 * kListCap + 4 * kDeferCap + 3 * 4 * kSlots
+  kListCap = 1536,
+  kDeferCap = 480,                               /* the replay's list (defer) */
+  kPoolBytes = 4 * kPoolWords + kOrderSpan / 8 + 2 * kListCap + 2 * kDeferCap
 };
-constexpr uint32_t kSlotDry = 0xffffffffu;       /* slot_lo: no piece left */
 static_assert(idx2(S_DONE, 0) == kPark, "parked lanes sit in DONE");
 
 /* LDS byte address of part q (16 B) of lane w's window inside the staging
@@ -421,12 +413,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     }
   }
   const uint64_t o_lo = pool_dry ? 0 : p.offsets[wg_lo], o_hi = pool_dry ? 0 : p.offsets[wg_hi];
-  /* Balancing across workgroups (p.tail != 0, a batch below 4 GiB): the last
-   * p.tail requests of every even range are pieces any workgroup may take
-   * once its own part is done; windows are then addressed from the batch
-   * start, so a lane's requests may come from anywhere in the batch. */
-  const bool steal_on = p.tail != 0u;
-  const uint64_t base = steal_on ? 0u : o_lo & ~(uint64_t) 3;
+  const uint64_t base = o_lo & ~(uint64_t) 3;
   if (o_hi - base >= 0xFFFF0000ull) {
     /* The window offsets below are u32 from `base`: a workgroup whose range
      * spans ~4 GiB (a request of that size among its requests) parses its
@@ -485,71 +472,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #pragma unroll
   for (int w = 0; w < (int) kEvWords; w++) ev[w] = evp[w] = 0;
 
-  /* the tail pieces this workgroup took: state (0 free, 1 being taken, 2
-   * ready), first request (kSlotDry: none left), request count */
-  uint32_t *slot_state = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(long_bits) + kOrderSpan / 8 +
-                                                      2 * kListCap + 4 * kDeferCap);
-  uint32_t *slot_lo = slot_state + kSlots, *slot_n = slot_state + 2 * kSlots;
-  /* own_n: requests of the range its owner hands out itself (the range minus
-   * its published tail); set once the range is known to be even or uneven */
-  uint32_t own_n = wg_hi - wg_lo;
-
-  /* The tail of range [lo, hi): what its owner publishes, decided from the
-   * range alone (the owner's even/uneven test below, repeated by the
-   * workgroup that takes a piece of it).  Wave-uniform; all lanes active. */
-  auto tail_of = [&](uint32_t lo, uint32_t hi) -> uint32_t {
-    const uint32_t sn = hi - lo;
-    if (sn < p.tail + (uint32_t) (WAVES * 64)) return 0u;
-    if (!(sn <= kOrderSpan && sn > (uint32_t) (WAVES * 64))) return p.tail;
-    const uint32_t *so = reinterpret_cast<const uint32_t *>(p.offsets + lo + min(lane, sn - 1u));
-    const uint32_t a0 = *GLOBAL(const uint32_t, so), a1 = *GLOBAL(const uint32_t, so + 2);
-    const uint64_t olo = p.offsets[lo], ohi = p.offsets[hi];
-    return __builtin_amdgcn_ballot_w64((uint64_t) (a1 - a0) * sn > 2u * (ohi - olo)) != 0 ? 0u : p.tail;
-  };
-  /* Slot s of this workgroup's taken pieces: its first request, kSlotDry when
-   * the batch has no piece left.  The first wave to need it takes the next
-   * piece from the global counter (tail pieces are numbered owner-major in
-   * k % grid, so consecutive takes spread over the owners); the others wait
-   * in LDS.  Wave-uniform. */
-  auto slot_get = [&](uint32_t sl) -> uint32_t {
-    uint32_t state = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(&slot_state[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if (state != 2u) {
-      uint32_t won = 0;
-      if (lane == 0) won = atomicCAS(&slot_state[sl], 0u, 1u) == 0u;
-      won = __builtin_amdgcn_readfirstlane(won);
-      if (won) {
-        uint32_t lo = kSlotDry, cnt = 0;
-        for (;;) {
-          uint32_t k = 0;
-          if (lane == 0) k = __hip_atomic_fetch_add(p.work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          k = __builtin_amdgcn_readfirstlane(k);
-          if (k >= gridDim.x * p.tail_pieces) break;
-          const uint32_t owner = k % gridDim.x, piece = k / gridDim.x;
-          const uint32_t olo = min(owner * p.span, p.n), ohi = min(olo + p.span, p.n);
-          const uint32_t tl = tail_of(olo, ohi);
-          const uint32_t clo = ohi - tl + piece * kPiece;
-          if (tl != 0u && clo < ohi) {
-            lo = clo;
-            cnt = min((uint32_t) kPiece, ohi - clo);
-            break;
-          }
-        }
-        if (lane == 0) {
-          slot_lo[sl] = lo;
-          slot_n[sl] = cnt;
-          __hip_atomic_store(&slot_state[sl], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      } else {
-        while (__builtin_amdgcn_readfirstlane(
-                   __hip_atomic_load(&slot_state[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 2u)
-          __builtin_amdgcn_s_sleep(2);
-      }
-    }
-    return __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(&slot_lo[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-  };
-
   /* give every lane without a pending request one from the pool; the offsets
    * loads are only consumed at the top of the next block */
   auto take = [&](uint32_t i) {
@@ -575,34 +497,16 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (!pend_ok && b0 + rank < nl) take(wg_lo + long_list[b0 + rank]);
       want = __ballot(!pend_ok);
     }
-    /* the range in order, skipping the listed requests (a few rounds at
-     * most), then (balancing on) the taken tail pieces: the counter runs on
-     * past own_n into slot (v - own_n) / kPiece */
+    /* the range in order, skipping the listed requests (a few rounds at most) */
     while (want && !pool_dry) {
       const uint32_t cnt = (uint32_t) __popcll(want);
       uint32_t b0 = 0;
       if (lane == 0) b0 = atomicAdd(wg_counter, cnt);
-      b0 = __builtin_amdgcn_readfirstlane(b0);
-      if (!steal_on && b0 + cnt >= own_n) pool_dry = true;
+      b0 = wg_lo + __builtin_amdgcn_readfirstlane(b0);
+      if (b0 + cnt >= wg_hi) pool_dry = true;
       const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
-      const uint32_t v = b0 + rank;
-      if (!pend_ok && v < own_n && !(listed && ((long_bits[v >> 5] >> (v & 31)) & 1u))) take(wg_lo + v);
-      if (steal_on && b0 + cnt > own_n) {
-        const uint32_t u0 = b0 > own_n ? b0 - own_n : 0u, u1 = b0 + cnt - own_n;
-        for (uint32_t sl = u0 / kPiece; sl <= (u1 - 1u) / kPiece; sl++) {
-          if (sl >= kSlots) {
-            pool_dry = true;
-            break;
-          }
-          const uint32_t lo = slot_get(sl);
-          if (lo == kSlotDry) {
-            pool_dry = true;
-            break;
-          }
-          const uint32_t nn = slot_n[sl], u = v - own_n;
-          if (!pend_ok && v >= own_n && u / kPiece == sl && u % kPiece < nn) take(lo + u % kPiece);
-        }
-      }
+      const uint32_t i = b0 + rank, k = i - wg_lo;
+      if (!pend_ok && i < wg_hi && !(listed && ((long_bits[k >> 5] >> (k & 31)) & 1u))) take(i);
       want = __ballot(!pend_ok);
     }
   };
@@ -624,15 +528,15 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     }
   };
 
-  /* the replay's work list: requests finalize deferred (indices); on
-   * overflow the replay scans every request the workgroup handed out (its
-   * own part and the pieces it took) */
+  /* the replay's work list: requests finalize deferred, as offsets in the
+   * range (u16); on overflow (or ranges over 64K requests) the replay scans
+   * the whole range */
   uint32_t *defer_n = wg_counter + 5;
-  uint32_t *defer_list = reinterpret_cast<uint32_t *>(long_list + kListCap);
+  uint16_t *defer_list = long_list + kListCap;
   auto defer = [&](uint32_t i) {
     *wg_deferred = 1u;
     const uint32_t at = atomicAdd(defer_n, 1u);
-    if (at < kDeferCap) defer_list[at] = i;
+    if (at < kDeferCap) defer_list[at] = (uint16_t) (i - wg_lo);
   };
 
   /* ---- decode ----
@@ -1070,15 +974,12 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   }
   for (uint32_t k = tid; k < kPoolWords + kOrderSpan / 32; k += WAVES * 64)
     reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave)[k] = k == 0 ? first_n : 0u;
-  for (uint32_t k = tid; k < kSlots; k += WAVES * 64) slot_state[k] = 0u;
   wait_vm0();   /* the pending offsets */
 #ifdef RHP_STAMPS
   const unsigned long long rt_loads = __builtin_amdgcn_s_memrealtime();
 #endif
   const bool uneven =
       may_order && __builtin_amdgcn_ballot_w64((uint64_t) (s1 - s0) * span_n > 2u * (o_hi - o_lo)) != 0;
-  /* an even range publishes its tail (tail_of: the same decision) */
-  if (steal_on && !uneven && span_n >= p.tail + (uint32_t) (WAVES * 64)) own_n = span_n - p.tail;
   /* An uneven range runs on 12 of the 16 waves: its end is set by its longest
    * requests (each walked by one lane from the first iteration on), and with
    * fewer waves sharing the CU every iteration is shorter while the lanes'
@@ -1359,9 +1260,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       u32x4a4 hint;
       uint32_t f;
     };
-    auto head = [&](bool valid, uint32_t k) {
+    auto head = [&](uint32_t k) {
       Head h = {0, 0, u32x4a4{0u, 0u, 0u, 0u}, 0u};
-      if (valid) {
+      if (k < wg_hi) {
         h.off = p.offsets[k];
         h.end = p.offsets[k + 1];
         if (http) h.hint = *GLOBAL(const u32x4a4, &p.http[k]);
@@ -1391,34 +1292,16 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     unsigned long long c0 = 0, c1 = 0;
     RHP_STAMP(c0);
 #endif
-    /* the deferred requests: the list finalize kept, or when it overflowed
-     * every request the workgroup handed out: its own part, then the tail
-     * pieces it took (slots 0.. up to the first empty one; no wave is taking
-     * one any more) */
+    /* the deferred requests: the list finalize kept, or the whole range when
+     * it overflowed */
     const uint32_t nd = *defer_n;
-    const bool use_list = nd <= kDeferCap;
-    uint32_t n_taken = 0;
-    if (!use_list)
-      while (n_taken < kSlots && slot_state[n_taken] == 2u && slot_lo[n_taken] != kSlotDry) n_taken++;
-    const uint32_t cnt = use_list ? nd : own_n + n_taken * kPiece;
-    auto req_at = [&](uint32_t k, bool &valid) -> uint32_t {
-      valid = k < cnt;
-      if (!valid) return 0u;
-      if (use_list) return defer_list[k];
-      if (k < own_n) return wg_lo + k;
-      const uint32_t u = k - own_n, sl = u / kPiece;
-      valid = u % kPiece < slot_n[sl];
-      return slot_lo[sl] + u % kPiece;
-    };
-    auto head_at = [&](uint32_t k) {
-      bool valid;
-      const uint32_t i = req_at(k, valid);
-      return head(valid, i);
-    };
+    const bool use_list = nd <= kDeferCap && wg_hi - wg_lo <= 65536u;
+    const uint32_t cnt = use_list ? nd : wg_hi - wg_lo;
+    auto req_at = [&](uint32_t k) { return wg_lo + (use_list ? (uint32_t) defer_list[k] : k); };
+    auto head_at = [&](uint32_t k) { return head(k < cnt ? req_at(k) : wg_hi); };
     Head nx = head_at(tid);
     for (uint32_t k = tid; k < cnt; k += WAVES * 64) {
-      bool valid;
-      const uint32_t i = req_at(k, valid);
+      const uint32_t i = req_at(k);
       const Head cur = nx;
       nx = head_at(k + WAVES * 64);
       const uint32_t f = what(cur);
@@ -1447,7 +1330,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const uint32_t ns = min(*slow_n, kSlowCap);
     for (uint32_t k = tid; k < ns; k += WAVES * 64) {
       const uint32_t i = slow[k];
-      finish_slow(i, head(true, i));
+      finish_slow(i, head(i));
 #ifdef RHP_STAMPS
       rp[2] += __popcll(__builtin_amdgcn_ballot_w64(true));
 #endif
@@ -1456,18 +1339,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     RHP_STAMP(c1);
     rp[0] += c1 - c0;
 #endif
-  }
-  if (steal_on) {
-    /* every wave is past its last piece take: the workgroup is done with the
-     * counters; the last one leaves them zeroed for the next launch (rhp.h) */
-    __syncthreads();
-    if (tid == 0) {
-      const uint32_t d = __hip_atomic_fetch_add(p.work + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (d == gridDim.x - 1u) {
-        __hip_atomic_store(p.work, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(p.work + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
   }
 #ifdef RHP_STAMPS
   if (lane == 0) {
@@ -1510,12 +1381,8 @@ int device_cus(int dev, int *cus)
   return 0;
 }
 
-#ifndef RHP_TAIL_DIV
-#define RHP_TAIL_DIV 4   /* the published tail: 1/RHP_TAIL_DIV of every range */
-#endif
-
 template <int WAVES, bool LATE, bool HTTP>
-int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus, uint64_t bytes_size)
+int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
 {
   const size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes;
   const uint32_t bit = 1u << (4 * (WAVES / 4) + (LATE ? 2 : 0) + (HTTP ? 1 : 0));
@@ -1530,20 +1397,9 @@ int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus, uint64_t byte
   uint32_t grid = (uint32_t) cus;
   uint32_t need = (prm.n + 64 * WAVES - 1) / (64 * WAVES);
   if (grid > need) grid = need > 0 ? need : 1;
-  /* each workgroup owns a contiguous n/grid share of the requests; with a
-   * work area and a batch below 4 GiB (windows addressed from the batch
-   * start), the last 1/RHP_TAIL_DIV of every even range is shared */
+  /* each workgroup owns a contiguous n/grid share of the requests */
   Params q = prm;
   q.span = (prm.n + grid - 1) / grid;
-  q.tail = 0;
-  q.tail_pieces = 0;
-  if (prm.work && grid >= 2 && bytes_size <= 0xFFFF0000ull) {
-    const uint32_t t = (q.span / RHP_TAIL_DIV) & ~63u;
-    if (t >= 64u) {
-      q.tail = t;
-      q.tail_pieces = (t + kPiece - 1) / kPiece;
-    }
-  }
   hipLaunchKernelGGL((rhp_dfa_kernel<WAVES, LATE, HTTP>), dim3(grid), dim3(WAVES * 64), lds_bytes, s, q);
   return (int) hipGetLastError();
 }
@@ -1612,7 +1468,6 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.hdrs = b->hdrs;
   prm.http = b->http;
   prm.last_len = b->last_len;
-  prm.work = b->work;
   prm.n = b->n;
   prm.max_headers = b->max_headers;
   prm.mode = b->mode;
@@ -1630,9 +1485,9 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
     return (int) hipGetLastError();
   }
   const bool late = late_issue(b->mode);
-  if (b->mode == RHP_MODE_HTTP) return launch_dfa<16, true, true>(prm, s, dev, cus, b->bytes_size);
-  if (late) return launch_dfa<16, true, false>(prm, s, dev, cus, b->bytes_size);
-  return launch_dfa<16, false, false>(prm, s, dev, cus, b->bytes_size);
+  if (b->mode == RHP_MODE_HTTP) return launch_dfa<16, true, true>(prm, s, dev, cus);
+  if (late) return launch_dfa<16, true, false>(prm, s, dev, cus);
+  return launch_dfa<16, false, false>(prm, s, dev, cus);
 }
 
 }  // extern "C"

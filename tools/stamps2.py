@@ -13,9 +13,13 @@ lib.rhp_debug_stamps.argtypes = [ctypes.c_void_p]
 # section names: early-issue kernel (phr mode) / late-issue kernel (http mode)
 names = ["A wait window / + framing finish", "C-E switch/refill/issue / C-D switch/refill",
          "decode / decode + finalize", "walk", "finalize/handover / issue"]
+NREQ = int(os.environ.get("STAMPS_N", 1 << 20))
+ONLY = os.environ.get("STAMPS_CFG")
 for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, 1), (rhp.GEN_ZIPF, 0x5EED0003, 32, 0, 0),
                                       (rhp.GEN_POST1K, 0x5EED0005, 16, 1, 1)):
-    buf, off = rhp.generate(cfg, 1 << 20, seed)
+    if ONLY and str(cfg) not in ONLY.split(","):
+        continue
+    buf, off = rhp.generate(cfg, NREQ, seed)
     dbs = [rhp.DeviceBatch(buf, off, maxh, mode, layout=layout) for _ in range(4)]
     for c in dbs[1:]:
         c.reqs, c.hdrs, c.http = dbs[0].reqs, dbs[0].hdrs, dbs[0].http

@@ -301,7 +301,7 @@ struct server_session
   server_t       *server;
   list_t          link;       /* in server->sessions */
   list_t          queued;     /* in server->queue (self-linked when not queued) */
-  bool            exact;      /* next batch: parse the remainder as one piece */
+  bool            exact;      /* unused (kept for the struct's layout) */
   bool            in_round;   /* taking part in the running batch round */
   bool            dead;       /* freed while in a round (the round releases it) */
 };

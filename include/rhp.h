@@ -88,7 +88,9 @@ enum rhp_layout {
 /* http_read_request result (24 B), RHP_MODE_HTTP only */
 typedef struct rhp_http {
   int32_t  result;         /* 1 ready, 0 need more bytes / empty, -1 malformed, RHP_RET_TOOLONG */
-  uint32_t body_kind;      /* 0: data_null(); 1: body = (req.ret, body_len) */
+  uint32_t body_kind;      /* 0: data_null(); 1: body = (req.ret, body_len);
+                              RHP_BODY_CHUNKED_PENDING: a speculative batch's chunked body,
+                              validated, not yet de-framed (rhp_fixup_sessions finishes it) */
   uint64_t consumed;       /* bytes stream_consume() is given (mod 2^64, http.c:216) */
   uint64_t body_len;
 } rhp_http_t;
@@ -111,6 +113,8 @@ typedef struct rhp_batch {
   uint32_t       *work;        /* reserved, may be NULL (device scratch of RHP_WORK_WORDS u32
                                   for future kernels; the current ones keep their scheduling
                                   state in LDS) */
+  uint32_t        flags;       /* RHP_BATCH_* */
+  uint32_t        reserved;
   const uint64_t *last_len;    /* device [n] or NULL (= all 0), RHP_MODE_PHR only:
                                   phr_parse_request's last_len per request
                                   (picohttpparser.c:383, 399-401): when last_len[i] != 0 the
@@ -120,12 +124,55 @@ typedef struct rhp_batch {
 } rhp_batch_t;
 
 #define RHP_WORK_WORDS 64u
+#define RHP_BODY_CHUNKED_PENDING 2u
+
+/* rhp_batch_t.flags */
+#define RHP_BATCH_SPECULATIVE 1u   /* RHP_MODE_HTTP: the requests may be speculative pieces of
+                                      pipelined input (rhp_fixup_sessions below): nothing is
+                                      written to bytes_rw (chunked bodies are validated and
+                                      left framed, body_kind RHP_BODY_CHUNKED_PENDING) */
 
 /* Parse a batch on `stream` (hipStream_t) of the calling thread's current
  * device.  Returns 0 on successful launch, a negative errno-style code for bad
  * arguments, or a positive hipError_t.  Thread-safe: one host thread per GPU
  * may call it concurrently (per-device state is cached per device id). */
 int rhp_parse_batch(const rhp_batch_t *batch, void *stream);
+
+/*
+ * Pipelined input (the reference's server_session_read loop,
+ * /root/reference/src/reactor/server.c:37-65, advancing by http.c:200, 216, 232).
+ * A session's unconsumed input is split by the caller at every empty line (the
+ * end of a header section: LF LF or LF CR LF) into pieces that are consecutive
+ * requests of a RHP_BATCH_SPECULATIVE http batch, so every request's header
+ * section ends a piece (#pieces >= #requests).  After rhp_parse_batch,
+ * rhp_fixup_sessions walks each session in order, as http_read_request would be
+ * called in a loop over the whole input: a piece that starts at the next request
+ * boundary and whose result cannot change with more input (1 within the piece,
+ * -1, RHP_RET_TOOLONG, or 0 for the session's last piece) is taken (a pending
+ * chunked body is de-framed in place now); anything else (a body that ran past
+ * its piece, a piece that started inside a body) is parsed again from the true
+ * boundary over the rest of the session's input.  Request m of a session is
+ * left in record slot piece_lo + m (reqs/hdrs/http of the batch), its start
+ * in req_start[piece_lo + m].  One launch, one thread per session.
+ */
+typedef struct rhp_session {
+  uint32_t piece_lo, piece_hi;   /* the session's pieces: requests [piece_lo, piece_hi) of the
+                                    batch, its bytes [offsets[piece_lo], offsets[piece_hi]) */
+} rhp_session_t;
+
+typedef struct rhp_session_result {
+  uint32_t n_slots;   /* record slots filled: every one but the last has result 1; the last
+                         one's result says where the session stopped (1: input used up) */
+  uint32_t more;      /* 1: more requests than pieces (a split the caller missed): the rest
+                         from offsets[piece_lo] + consumed needs another batch */
+  uint64_t consumed;  /* bytes of the session's input taken by its result-1 requests */
+} rhp_session_result_t;
+
+/* Launch status as rhp_parse_batch.  `batch` is the speculative batch already
+ * parsed on `stream`; sessions, results and req_start (u64 [n]) are device
+ * memory. */
+int rhp_fixup_sessions(const rhp_batch_t *batch, const rhp_session_t *sessions, uint32_t n_sessions,
+                       rhp_session_result_t *results, uint64_t *req_start, void *stream);
 
 /* Which kernel implementation rhp_parse_batch uses (diagnostics / A-B tests). */
 enum rhp_impl {

@@ -30,6 +30,10 @@ extern "C" {
 #endif
 
 int rhp_cpu_parse_batch(const rhp_batch_t *batch);
+/* rhp_fixup_sessions (rhp.h) on the host, over a RHP_BATCH_SPECULATIVE batch
+ * parsed by rhp_cpu_parse_batch; 0 or -22 */
+int rhp_cpu_fixup_sessions(const rhp_batch_t *batch, const rhp_session_t *sessions, uint32_t n_sessions,
+                           rhp_session_result_t *results, uint64_t *req_start);
 int rhp_emu_parse_batch(const rhp_batch_t *batch, uint64_t *stats);
 
 /* struct phr_header (picohttpparser.h:42-47): name == NULL for an obs-fold line */

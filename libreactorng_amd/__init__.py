@@ -49,13 +49,21 @@ class Batch(ctypes.Structure):
                 ("bytes_size", ctypes.c_uint64), ("n", ctypes.c_uint32), ("max_headers", ctypes.c_uint32),
                 ("mode", ctypes.c_uint32), ("layout", ctypes.c_uint32), ("reqs", ctypes.c_void_p),
                 ("hdrs", ctypes.c_void_p), ("http", ctypes.c_void_p), ("work", ctypes.c_void_p),
-                ("last_len", ctypes.c_void_p)]
+                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("last_len", ctypes.c_void_p)]
+
+
+BATCH_SPECULATIVE = 1        # rhp_batch_t.flags (rhp.h RHP_BATCH_SPECULATIVE)
+BODY_CHUNKED_PENDING = 2
+SESSION_DTYPE = np.dtype([("piece_lo", "<u4"), ("piece_hi", "<u4")])
+SESSION_RESULT_DTYPE = np.dtype([("n_slots", "<u4"), ("more", "<u4"), ("consumed", "<u8")])
 
 
 # exported C-ABI symbols of librhp.so, as declared in include/rhp.h
-RHP_SYMBOLS = ("rhp_parse_batch", "rhp_set_impl", "rhp_kernel_name", "rhp_version", "rhp_write_responses")
+RHP_SYMBOLS = ("rhp_parse_batch", "rhp_set_impl", "rhp_kernel_name", "rhp_version", "rhp_write_responses",
+               "rhp_fixup_sessions")
 HOST_SYMBOLS = ("rhp_gen_size", "rhp_gen_fill", "rhp_gen_header_bytes", "rhp_splitmix64",
-                "rhp_emu_parse_batch", "rhp_cpu_parse_batch", "rhp_phr_parse_request", "rhp_http_read_cpu")
+                "rhp_emu_parse_batch", "rhp_cpu_parse_batch", "rhp_phr_parse_request", "rhp_http_read_cpu",
+                "rhp_cpu_fixup_sessions")
 
 _rhp = None
 _host = None
@@ -115,6 +123,8 @@ def host() -> ctypes.CDLL:
         _host.rhp_phr_parse_request.restype = ctypes.c_int
         _host.rhp_http_read_cpu.argtypes = [vp, sz, P(HttpReq), P(PhrHeader), P(sz)]
         _host.rhp_http_read_cpu.restype = ctypes.c_int
+        _host.rhp_cpu_fixup_sessions.argtypes = [ctypes.POINTER(Batch), vp, ctypes.c_uint32, vp, vp]
+        _host.rhp_cpu_fixup_sessions.restype = ctypes.c_int
     return _host
 
 
@@ -203,14 +213,14 @@ def hdr_view(flat: np.ndarray, n: int, max_headers: int, layout: int) -> np.ndar
     return flat[: n * max_headers].reshape(n, max_headers)
 
 
-def _host_batch(buf, off, max_headers, mode, layout=LAYOUT_REQUEST_MAJOR, last_len=None):
+def _host_batch(buf, off, max_headers, mode, layout=LAYOUT_REQUEST_MAJOR, last_len=None, flags=0):
     n = len(off) - 1
     reqs = np.zeros(n, dtype=REQ_DTYPE)
     hdrs = np.zeros(max(max_headers * n, 1), dtype=HDR_DTYPE)
     http = np.zeros(n, dtype=HTTP_DTYPE)
     rw = buf.copy()
     b = Batch(_ptr(rw), _ptr(rw), _ptr(off), rw.size, n, max_headers, mode, layout, _ptr(reqs), _ptr(hdrs),
-              _ptr(http), 0, _ptr(last_len) if last_len is not None else None)
+              _ptr(http), 0, flags, 0, _ptr(last_len) if last_len is not None else None)
     return b, Result(reqs, hdr_view(hdrs, n, max_headers, layout), http if mode == MODE_HTTP else None, rw)
 
 
@@ -240,7 +250,8 @@ class DeviceBatch:
     """A batch resident in HBM plus its output buffers (torch tensors as plumbing)."""
 
     def __init__(self, buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,
-                 device: str = "cuda", layout: int = LAYOUT_REQUEST_MAJOR, last_len: np.ndarray | None = None):
+                 device: str = "cuda", layout: int = LAYOUT_REQUEST_MAJOR, last_len: np.ndarray | None = None,
+                 flags: int = 0):
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("no GPU visible: the rhp product path runs on MI355X only")
@@ -248,6 +259,7 @@ class DeviceBatch:
         self.max_headers = max_headers
         self.mode = mode
         self.layout = layout
+        self.flags = flags
         self.bytes = torch.from_numpy(buf).to(device)
         self.offsets = torch.from_numpy(off.view(np.int64)).to(device)
         self.reqs = torch.zeros(self.n * REQ_DTYPE.itemsize, dtype=torch.uint8, device=device)
@@ -262,7 +274,7 @@ class DeviceBatch:
     def desc(self) -> Batch:
         return Batch(self.bytes.data_ptr(), self.bytes.data_ptr(), self.offsets.data_ptr(), self.bytes.numel(),
                      self.n, self.max_headers, self.mode, self.layout, self.reqs.data_ptr(), self.hdrs.data_ptr(),
-                     self.http.data_ptr(), self.work.data_ptr(),
+                     self.http.data_ptr(), self.work.data_ptr(), self.flags, 0,
                      self.last_len.data_ptr() if self.last_len is not None else None)
 
     def launch(self, stream=None) -> None:
@@ -291,6 +303,97 @@ def parse_batch(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: i
         db = DeviceBatch(buf, off, max_headers, mode, layout=layout, last_len=last_len)
         db.launch()
         return db.result()
+    finally:
+        lib().rhp_set_impl(IMPL_DFA)
+
+
+# ---------------------------------------------------------------------------
+# Pipelined input (rhp.h rhp_fixup_sessions; the reference's server_session_read
+# loop, /root/reference/src/reactor/server.c:37-65): a session's bytes split at
+# every empty line into pieces, parsed speculatively, then walked in order.
+
+def split_pieces(data: bytes):
+    """Piece lengths of one session's input: a cut after every empty line (LF LF
+    or LF CR LF, where a header section can end) and at the end."""
+    cuts, n = [], len(data)
+    p = data.find(b"\n")
+    while p != -1:
+        q = p + 1
+        if q < n and data[q] == 10:
+            cuts.append(q + 1)
+        elif q + 1 < n and data[q] == 13 and data[q + 1] == 10:
+            cuts.append(q + 2)
+        p = data.find(b"\n", p + 1)
+    out, at = [], 0
+    for c in cuts:
+        if c > at and c < n:
+            out.append(c - at)
+            at = c
+    if at < n or not out:
+        out.append(n - at)
+    return out
+
+
+def pack_sessions(sessions, split: bool = True):
+    """(buf, piece offsets, rhp_session_t array, session byte starts) for a list
+    of session inputs packed back to back (split=False: one piece per session)."""
+    pieces, sess, starts, at = [], [], [], 0
+    for data in sessions:
+        lo = len(pieces)
+        starts.append(at)
+        for ln in (split_pieces(data) if split else [len(data)]):
+            pieces.append((at, ln))
+            at += ln
+        sess.append((lo, len(pieces)))
+    off = np.zeros(len(pieces) + 1, dtype=np.uint64)
+    for i, (a, ln) in enumerate(pieces):
+        off[i] = a
+    off[len(pieces)] = at
+    buf = np.zeros(at + RHP_PAD, dtype=np.uint8)
+    if at:
+        buf[:at] = np.frombuffer(b"".join(sessions), dtype=np.uint8)
+    ss = np.zeros(len(sess), dtype=SESSION_DTYPE)
+    for i, (lo, hi) in enumerate(sess):
+        ss[i] = (lo, hi)
+    return buf, off, ss, np.array(starts, dtype=np.uint64)
+
+
+def fixup_cpu(buf, off, sessions, max_headers: int = 16, emulate_dfa: bool = False, layout: int = LAYOUT_REQUEST_MAJOR):
+    """Speculative http batch (host exact parser, or the kernel's DFA emulation)
+    + rhp_cpu_fixup_sessions.  Returns (Result, session results, req_start)."""
+    b, res = _host_batch(buf, off, max_headers, MODE_HTTP, layout, None, BATCH_SPECULATIVE)
+    if emulate_dfa:
+        rc = host().rhp_emu_parse_batch(ctypes.byref(b), None)
+    else:
+        rc = host().rhp_cpu_parse_batch(ctypes.byref(b))
+    if rc != 0:
+        raise RuntimeError(f"host parse failed: {rc}")
+    out = np.zeros(len(sessions), dtype=SESSION_RESULT_DTYPE)
+    starts = np.zeros(max(len(off) - 1, 1), dtype=np.uint64)
+    rc = host().rhp_cpu_fixup_sessions(ctypes.byref(b), _ptr(sessions), len(sessions), _ptr(out), _ptr(starts))
+    if rc != 0:
+        raise RuntimeError(f"rhp_cpu_fixup_sessions failed: {rc}")
+    return res, out, starts
+
+
+def fixup_gpu(buf, off, sessions, max_headers: int = 16, impl: int = IMPL_DFA, layout: int = LAYOUT_REQUEST_MAJOR):
+    """Speculative http batch on the GPU + rhp_fixup_sessions, one stream."""
+    import torch
+    lib().rhp_set_impl(impl)
+    try:
+        db = DeviceBatch(buf, off, max_headers, MODE_HTTP, layout=layout, flags=BATCH_SPECULATIVE)
+        db.launch()
+        ds = torch.from_numpy(sessions.view(np.uint8).copy()).to("cuda")
+        dres = torch.zeros(len(sessions) * SESSION_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        dst = torch.zeros(max(db.n, 1) * 8, dtype=torch.uint8, device="cuda")
+        d = db.desc()
+        rc = lib().rhp_fixup_sessions(ctypes.byref(d), ctypes.c_void_p(ds.data_ptr()), len(sessions),
+                                      ctypes.c_void_p(dres.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
+                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"rhp_fixup_sessions failed: {rc}")
+        res = db.result()
+        return res, dres.cpu().numpy().view(SESSION_RESULT_DTYPE), dst.cpu().numpy().view(np.uint64)
     finally:
         lib().rhp_set_impl(IMPL_DFA)
 

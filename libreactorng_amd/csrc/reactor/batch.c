@@ -51,8 +51,12 @@ typedef struct slot
   rhp_req_t   *h_req;
   rhp_hdr_t   *h_hdr;
   rhp_http_t  *h_http;
-  void        *d_bytes, *d_off, *d_req, *d_hdr, *d_http;
-  uint32_t     n;
+  uint64_t    *h_start;      /* rhp_fixup_sessions: where each record slot's request starts */
+  rhp_session_t        *h_sess;
+  rhp_session_result_t *h_sres;
+  size_t       cap_sess;
+  void        *d_bytes, *d_off, *d_req, *d_hdr, *d_http, *d_start, *d_sess, *d_sres;
+  uint32_t     n, n_sess;
   size_t       bytes;
   uint64_t     t_submit;
 } slot_t;
@@ -220,10 +224,28 @@ static void dev_free(void **p)
   *p = NULL;
 }
 
-uint8_t *reactor_batch_reserve(int k, size_t bytes, uint32_t n)
+uint8_t *reactor_batch_reserve(int k, size_t bytes, uint32_t n, uint32_t n_sessions)
 {
   (void) parser();
   slot_t *s = &B.slot[k];
+  if (n_sessions > s->cap_sess)
+  {
+    size_t c = s->cap_sess ? s->cap_sess : 1024;
+    while (c < n_sessions)
+      c *= 2;
+    host_free(s->h_sess);
+    host_free(s->h_sres);
+    s->h_sess = host_alloc(c * sizeof *s->h_sess);
+    s->h_sres = host_alloc(c * sizeof *s->h_sres);
+    if (B.parser == PARSER_GPU)
+    {
+      dev_free(&s->d_sess);
+      dev_free(&s->d_sres);
+      HIP(hipMalloc(&s->d_sess, c * sizeof *s->h_sess));
+      HIP(hipMalloc(&s->d_sres, c * sizeof *s->h_sres));
+    }
+    s->cap_sess = c;
+  }
   const size_t need = bytes + RHP_PAD;
   if (need > s->cap_bytes)
   {
@@ -250,6 +272,8 @@ uint8_t *reactor_batch_reserve(int k, size_t bytes, uint32_t n)
     host_free(s->h_req);
     host_free(s->h_hdr);
     host_free(s->h_http);
+    host_free(s->h_start);
+    s->h_start = host_alloc(c * sizeof *s->h_start);
     s->h_off = host_alloc(c * sizeof *s->h_off);
     s->h_req = host_alloc(c * sizeof *s->h_req);
     s->h_hdr = host_alloc(c * REACTOR_BATCH_HEADERS * sizeof *s->h_hdr);
@@ -260,6 +284,8 @@ uint8_t *reactor_batch_reserve(int k, size_t bytes, uint32_t n)
       dev_free(&s->d_req);
       dev_free(&s->d_hdr);
       dev_free(&s->d_http);
+      dev_free(&s->d_start);
+      HIP(hipMalloc(&s->d_start, c * sizeof *s->h_start));
       HIP(hipMalloc(&s->d_off, c * sizeof *s->h_off));
       HIP(hipMalloc(&s->d_req, c * sizeof *s->h_req));
       HIP(hipMalloc(&s->d_hdr, c * REACTOR_BATCH_HEADERS * sizeof *s->h_hdr));
@@ -280,6 +306,11 @@ uint64_t *reactor_batch_offsets(int k)
   return B.slot[k].h_off;
 }
 
+rhp_session_t *reactor_batch_sessions(int k)
+{
+  return B.slot[k].h_sess;
+}
+
 /* runs on a HIP runtime thread once the round's copies have landed: wake the
  * reactor loop (write(2) on an eventfd; no HIP call here) */
 static void round_done(void *arg)
@@ -294,14 +325,17 @@ static void host_parse(batch_state_t *st, int k)
   slot_t *s = &st->slot[k];
   rhp_batch_t b = {
     .bytes = s->h_bytes, .bytes_rw = s->h_bytes, .offsets = s->h_off, .bytes_size = s->bytes + RHP_PAD, .n = s->n,
-    .max_headers = REACTOR_BATCH_HEADERS, .mode = RHP_MODE_HTTP, .reqs = s->h_req, .hdrs = s->h_hdr, .http = s->h_http};
+    .max_headers = REACTOR_BATCH_HEADERS, .mode = RHP_MODE_HTTP, .reqs = s->h_req, .hdrs = s->h_hdr, .http = s->h_http,
+    .flags = RHP_BATCH_SPECULATIVE};
   (void) rhp_cpu_parse_batch(&b);
+  (void) rhp_cpu_fixup_sessions(&b, s->h_sess, s->n_sess, s->h_sres, s->h_start);
 }
 
-void reactor_batch_submit(int k, uint32_t n, size_t bytes)
+void reactor_batch_submit(int k, uint32_t n, size_t bytes, uint32_t n_sessions)
 {
   slot_t *s = &B.slot[k];
   s->n = n;
+  s->n_sess = n_sessions;
   s->bytes = bytes;
   s->t_submit = B.stats ? now_ns() : 0;
   memset(s->h_bytes + bytes, 0, RHP_PAD);
@@ -326,17 +360,29 @@ void reactor_batch_submit(int k, uint32_t n, size_t bytes)
   }
   HIP(hipMemcpyAsync(s->d_bytes, s->h_bytes, bytes + RHP_PAD, hipMemcpyHostToDevice, B.stream));
   HIP(hipMemcpyAsync(s->d_off, s->h_off, (n + 1) * sizeof *s->h_off, hipMemcpyHostToDevice, B.stream));
+  HIP(hipMemcpyAsync(s->d_sess, s->h_sess, n_sessions * sizeof *s->h_sess, hipMemcpyHostToDevice, B.stream));
+  /* the pieces speculatively, then every session walked in order from its
+   * true request boundaries (include/rhp.h rhp_fixup_sessions): all of a
+   * round's pipelined requests, bodies included, in this one round */
   rhp_batch_t b = {
     .bytes = s->d_bytes, .bytes_rw = s->d_bytes, .offsets = s->d_off, .bytes_size = bytes + RHP_PAD, .n = n,
     .max_headers = REACTOR_BATCH_HEADERS, .mode = RHP_MODE_HTTP, .reqs = s->d_req, .hdrs = s->d_hdr, .http = s->d_http,
-    .work = B.d_work};
+    .work = B.d_work, .flags = RHP_BATCH_SPECULATIVE};
   int rc = rhp_parse_batch(&b, B.stream);
   if (rc != 0)
     die("rhp_parse_batch", rc);
+  rc = rhp_fixup_sessions(&b, s->d_sess, n_sessions, s->d_sres, s->d_start, B.stream);
+  if (rc != 0)
+    die("rhp_fixup_sessions", rc);
   HIP(hipMemcpyAsync(s->h_req, s->d_req, n * sizeof *s->h_req, hipMemcpyDeviceToHost, B.stream));
   HIP(hipMemcpyAsync(s->h_hdr, s->d_hdr, (size_t) n * REACTOR_BATCH_HEADERS * sizeof *s->h_hdr, hipMemcpyDeviceToHost,
                      B.stream));
   HIP(hipMemcpyAsync(s->h_http, s->d_http, n * sizeof *s->h_http, hipMemcpyDeviceToHost, B.stream));
+  HIP(hipMemcpyAsync(s->h_sres, s->d_sres, n_sessions * sizeof *s->h_sres, hipMemcpyDeviceToHost, B.stream));
+  HIP(hipMemcpyAsync(s->h_start, s->d_start, n * sizeof *s->h_start, hipMemcpyDeviceToHost, B.stream));
+  /* chunked bodies are de-framed in place (http.c:155) by the fix-up: the
+   * round's bytes come back with the records, one asynchronous copy */
+  HIP(hipMemcpyAsync(s->h_bytes, s->d_bytes, bytes, hipMemcpyDeviceToHost, B.stream));
   HIP(hipLaunchHostFunc(B.stream, round_done, (void *) (intptr_t) B.efd));
 }
 
@@ -364,19 +410,6 @@ void reactor_batch_wait(void)
 void reactor_batch_result(int k, reactor_batch_result_t *out)
 {
   slot_t *s = &B.slot[k];
-  if (B.parser == PARSER_GPU && !B.diag_host)
-  {
-    /* chunked bodies were de-framed in place in device memory (http.c:155):
-     * bring those bytes back so the caller sees the rewritten input (the
-     * round's work on the stream is complete: plain copies) */
-    for (uint32_t i = 0; i < s->n; i++)
-    {
-      const rhp_http_t *x = &s->h_http[i];
-      if (x->result == 1 && x->body_kind && x->consumed != (uint64_t) s->h_req[i].ret + x->body_len)
-        HIP(hipMemcpy(s->h_bytes + s->h_off[i], (uint8_t *) s->d_bytes + s->h_off[i], x->consumed,
-                      hipMemcpyDeviceToHost));
-    }
-  }
   if (B.stats)
   {
     B.st_rounds++;
@@ -389,6 +422,10 @@ void reactor_batch_result(int k, reactor_batch_result_t *out)
   out->n = s->n;
   out->http = s->h_http;
   out->offsets = s->h_off;
+  out->sessions = s->h_sess;
+  out->session_results = s->h_sres;
+  out->req_start = s->h_start;
+  out->n_sessions = s->n_sess;
 }
 
 enum { WRITER_HOST, WRITER_HOST_BATCH, WRITER_GPU };

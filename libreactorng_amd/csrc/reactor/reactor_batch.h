@@ -17,18 +17,28 @@ typedef struct reactor_batch_result
   const rhp_hdr_t  *hdrs;    /* REACTOR_BATCH_HEADERS per request, request-major */
   uint32_t          n;
   const rhp_http_t *http;
+  /* rhp_fixup_sessions: session m's requests are record slots
+   * sessions[m].piece_lo + 0 .. + session_results[m].n_slots - 1, request j
+   * starting at byte req_start[j] of `bytes` */
+  const rhp_session_t        *sessions;
+  const rhp_session_result_t *session_results;
+  const uint64_t             *req_start;
+  uint32_t                    n_sessions;
 } reactor_batch_result_t;
 
 /* 1: rounds complete asynchronously (gpu parser) and each completion adds 1 to
  * the eventfd reactor_batch_fd(); 0: reactor_batch_submit parses in place */
 int       reactor_batch_async(void);
 int       reactor_batch_fd(void);
-/* staging of slot k for `bytes` packed input bytes (+ RHP_PAD) and n segments */
-uint8_t  *reactor_batch_reserve(int k, size_t bytes, uint32_t n);
+/* staging of slot k for `bytes` packed input bytes (+ RHP_PAD), n pieces and
+ * n_sessions sessions */
+uint8_t  *reactor_batch_reserve(int k, size_t bytes, uint32_t n, uint32_t n_sessions);
 uint64_t *reactor_batch_offsets(int k);
-/* parse slot k's n segments (offsets[0..n-1], offsets[n] = bytes) in
- * http_read_request mode; slots complete in submission order */
-void      reactor_batch_submit(int k, uint32_t n, size_t bytes);
+rhp_session_t *reactor_batch_sessions(int k);
+/* parse slot k's n pieces (offsets[0..n-1], offsets[n] = bytes) of
+ * n_sessions sessions: a speculative http batch, then rhp_fixup_sessions;
+ * slots complete in submission order */
+void      reactor_batch_submit(int k, uint32_t n, size_t bytes, uint32_t n_sessions);
 /* rounds completed since the last call (reads the eventfd; 0 if none) */
 int       reactor_batch_completed(void);
 /* block until every submitted round is complete (teardown) */

@@ -20,13 +20,15 @@
  * the first parses; a session belongs to one round at a time.  Rounds complete
  * and dispatch in submission order.
  *
- * Pipelined input: a session's input is split
- * speculatively after every "\r\n\r\n" and each piece is one request of the
- * batch, so N pipelined requests cost one launch, not N.  A piece's result is
- * taken when it is the last piece (its length is the rest of the input, as
- * for http_read_request) or when it parsed as one complete request that ends
- * exactly at the next piece; otherwise (a body, LF-only line ends, ...) the
- * rest of that session's input is parsed again, whole, in the next batch.
+ * Pipelined input: a session's input is split after
+ * every empty line (LF LF, LF CR LF: where a header section can end) into
+ * pieces of one speculative batch, and the device's fix-up pass
+ * (include/rhp.h rhp_fixup_sessions) walks every session from its true
+ * request boundaries -- taking a piece's result where more input cannot change
+ * it, parsing again where a body ran past its piece -- so all of a round's
+ * pipelined requests, bodies (Content-Length, chunked) and LF-only line ends
+ * included, are parsed in that one round, as the reference's
+ * server_session_read loop (server.c:37-65) parses them in one pass.
  */
 #include <stddef.h>
 #include <stdio.h>
@@ -175,7 +177,6 @@ typedef struct piece
   uint64_t          start;   /* offset in the session's unconsumed input */
   uint64_t          len;
   uint32_t          index;   /* request index in the batch */
-  bool              last;
 } piece_t;
 
 typedef struct round
@@ -283,55 +284,56 @@ static void w_flush_round(round_t *r)
       stream_flush(&r->sessions[i]->stream);
 }
 
-static const uint8_t *find_crlfcrlf(const uint8_t *p, const uint8_t *end)
+/* the end of the first empty line at or after p (LF LF or LF CR LF: where a
+ * header section can end, picohttpparser.c:266-275), or NULL */
+static const uint8_t *find_empty_line(const uint8_t *p, const uint8_t *end)
 {
-  while (end - p >= 4)
+  while (p < end)
   {
-    const uint8_t *q = memchr(p + 3, '\n', (size_t) (end - p - 3));
-    if (!q)
+    const uint8_t *q = memchr(p, '\n', (size_t) (end - p));
+    if (!q || q + 1 >= end)
       return NULL;
-    if (q[-1] == '\r' && q[-2] == '\n' && q[-3] == '\r')
-      return q + 1;
-    p = q - 2;
+    if (q[1] == '\n')
+      return q + 2;
+    if (q[1] == '\r' && q + 2 < end && q[2] == '\n')
+      return q + 3;
+    p = q + 1;
   }
   return NULL;
 }
 
-/* dispatch the parsed pieces of one session in order; false: needs another
- * batch over the rest of its input */
-static bool server_session_dispatch(server_session_t *s, const piece_t *pc, size_t np,
+/* dispatch the requests the fix-up found in one session's input, in order
+ * (record slots lo, lo + 1, ...); false: the session needs another batch over
+ * the rest of its input */
+static bool server_session_dispatch(server_session_t *s, uint32_t lo, const rhp_session_result_t *sr,
                                     const reactor_batch_result_t *res)
 {
   bool abort = false;
-  uint64_t at = 0;
-  size_t k = 0;
+  uint32_t m = 0;
   bool more = false;
   while (s->flags & SERVER_SESSION_READY)
   {
     data_t in = stream_read(&s->stream);
-    if (k == np)
+    if (m == sr->n_slots)
     {
-      more = !data_empty(in);   /* requests left behind a trusted piece: parse the rest */
+      more = sr->more || !data_empty(in);   /* pieces ran out, or bytes that arrived during the round */
       break;
     }
-    const piece_t *p = &pc[k];
-    const rhp_http_t *x = &res->http[p->index];
-    if (p->start != at || !(p->last || (x->result == 1 && x->consumed == p->len)))
-    {
-      more = true;
-      break;
-    }
+    const uint32_t i = lo + m;
+    const rhp_http_t *x = &res->http[i];
     int result = x->result;
     size_t consumed = 0;
     if (result == RHP_RET_TOOLONG)
     {
       /* a header section the batch records cannot hold (> RHP_MAX_LEN): the
-       * pointer-based host parser answers for this request */
+       * pointer-based host parser answers for this request; the rest of the
+       * input goes to the next batch */
       s->request.fields_count = REACTOR_BATCH_HEADERS;
       const size_t before = data_size(in);
       result = http_read_request(&s->stream, &s->request.method, &s->request.target, &s->request.body,
                                  s->request.fields, &s->request.fields_count);
       consumed = before - data_size(stream_read(&s->stream));
+      more = true;
     }
     if (result == -1)
     {
@@ -342,18 +344,16 @@ static bool server_session_dispatch(server_session_t *s, const piece_t *pc, size
       break;
     if (x->result != RHP_RET_TOOLONG)
     {
-      const uint64_t off = res->offsets[p->index];
       uint8_t *base = data_base(in);
-      if (x->body_kind && x->consumed != (uint64_t) res->reqs[p->index].ret + x->body_len)
-        memcpy(base, res->bytes + off, x->consumed);   /* chunked body, de-framed in place */
-      reactor_http_fill(base, &res->reqs[p->index], res->hdrs + (size_t) p->index * REACTOR_BATCH_HEADERS, 1, x,
+      if (x->body_kind && x->consumed != (uint64_t) res->reqs[i].ret + x->body_len)
+        memcpy(base, res->bytes + res->req_start[i], x->consumed);   /* chunked body, de-framed in place */
+      reactor_http_fill(base, &res->reqs[i], res->hdrs + (size_t) i * REACTOR_BATCH_HEADERS, 1, x,
                         &s->request.method, &s->request.target, &s->request.body, s->request.fields,
                         &s->request.fields_count);
       consumed = x->consumed;
       stream_consume(&s->stream, consumed);
     }
-    at += consumed;
-    k++;
+    m++;
     s->flags &= ~SERVER_SESSION_READY;
     s->flags |= SERVER_SESSION_PROCESSING;
     s->abort = &abort;
@@ -362,7 +362,11 @@ static bool server_session_dispatch(server_session_t *s, const piece_t *pc, size
       return true;
     s->abort = NULL;
     s->flags &= ~SERVER_SESSION_PROCESSING;
+    if (more)
+      break;
   }
+  if (!(s->flags & SERVER_SESSION_READY) && m < sr->n_slots)
+    more = true;   /* an asynchronous reply: the rest is parsed again once the session is ready */
   if (!W.on)
     stream_flush(&s->stream);   /* round-batched replies: flushed after the round's write (w_flush_round) */
   return !more;
@@ -417,17 +421,16 @@ static bool round_build(server_t *server, round_t *r, size_t *bytes_out)
     const uint8_t *b = data_base(in), *end = b + data_size(in), *p = b;
     while (p < end)
     {
-      const uint8_t *q = s->exact ? NULL : find_crlfcrlf(p, end);
-      if (!q || q == end)
+      const uint8_t *q = find_empty_line(p, end);
+      if (!q)
         q = end;
       r->pieces = grow(r->pieces, &r->cap_pieces, r->n_pieces + 1, sizeof *r->pieces);
       const uint32_t index = (uint32_t) r->n_pieces;
       r->pieces[index] = (piece_t) {.session = s, .start = (uint64_t) (p - b), .len = (uint64_t) (q - p),
-                                    .index = index, .last = q == end};
+                                    .index = index};
       r->n_pieces = index + 1u;
       p = q;
     }
-    s->exact = false;
     bytes += data_size(in);
   }
   *bytes_out = bytes;
@@ -443,17 +446,13 @@ static void round_finish(round_t *r, int k, bool dispatch)
     reactor_batch_result(k, &res);
   size_t i = 0;
   W.on = dispatch && reactor_batch_writer();
-  for (size_t kk = 0; dispatch && i < r->n_sessions; i++)
+  /* batch session i is round session i (a session without input has no
+   * pieces and no request) */
+  for (; dispatch && r->n_pieces && i < r->n_sessions; i++)
   {
     server_session_t *s = r->sessions[i];
-    size_t k0 = kk;
-    while (kk < r->n_pieces && r->pieces[kk].session == s)
-      kk++;
-    if (!s->dead && !server_session_dispatch(s, r->pieces + k0, kk - k0, &res) && !s->dead)
-    {
-      s->exact = true;   /* parse the rest as one piece (exact http_read_request semantics) */
-      server_queue(s);
-    }
+    if (!s->dead && !server_session_dispatch(s, res.sessions[i].piece_lo, &res.session_results[i], &res) && !s->dead)
+      server_queue(s);   /* the rest of its input in a later batch */
   }
   if (W.on)
   {
@@ -541,18 +540,21 @@ static void server_batch_run(reactor_event_t *event)
   /* pack every session's input, back to back, and parse all pieces at once */
   if (r->n_pieces)
   {
-    uint8_t *h = reactor_batch_reserve(k, bytes, (uint32_t) r->n_pieces);
+    uint8_t *h = reactor_batch_reserve(k, bytes, (uint32_t) r->n_pieces, (uint32_t) r->n_sessions);
     uint64_t *off = reactor_batch_offsets(k);
+    rhp_session_t *ss = reactor_batch_sessions(k);
     size_t at = 0, q = 0;
     for (size_t i = 0; i < r->n_sessions; i++)
     {
       data_t in = stream_read(&r->sessions[i]->stream);
       memcpy(h + at, data_base(in), data_size(in));
+      ss[i].piece_lo = (uint32_t) q;
       for (; q < r->n_pieces && r->pieces[q].session == r->sessions[i]; q++)
         off[q] = at + r->pieces[q].start;
+      ss[i].piece_hi = (uint32_t) q;
       at += data_size(in);
     }
-    reactor_batch_submit(k, (uint32_t) r->n_pieces, bytes);
+    reactor_batch_submit(k, (uint32_t) r->n_pieces, bytes, (uint32_t) r->n_sessions);
   }
   if (round_stats)
   {

@@ -38,7 +38,11 @@ void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
   const uint64_t hs_req = b->layout == RHP_LAYOUT_HEADER_MAJOR ? 1u : b->max_headers;
   const uint64_t hs_hdr = b->layout == RHP_LAYOUT_HEADER_MAJOR ? b->n : 1u;
   rhp_hdr_t *h = b->hdrs + i * hs_req;
-  if (b->mode == RHP_MODE_HTTP) scalar_http(b->bytes_rw + off, len, b->max_headers, &r, h, hs_hdr, &b->http[i]);
+  if (b->mode == RHP_MODE_HTTP) {
+    PlainBytes B{b->bytes_rw + off};
+    scalar_http_t(B, b->bytes_rw + off, len, b->max_headers, &r, h, hs_hdr, &b->http[i],
+                  !(b->flags & RHP_BATCH_SPECULATIVE));
+  }
   else {
     const uint64_t ll = b->last_len ? b->last_len[i] : 0;
     const int pre = ll ? is_complete(b->bytes + off, len, ll) : 0;   /* picohttpparser.c:399-401 */
@@ -140,7 +144,8 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
         r.num_headers = (uint16_t) d.nh;
         r.flags = 0;
         b->reqs[i] = r;
-        if (b->mode == RHP_MODE_HTTP) http_frame(b->bytes_rw + off, len, r, hout, hs_hdr, &b->http[i]);
+        if (b->mode == RHP_MODE_HTTP)
+          http_frame(b->bytes_rw + off, len, r, hout, hs_hdr, &b->http[i], ~0ull, !(b->flags & RHP_BATCH_SPECULATIVE));
       } else if (bad) {
         st_count.fast_bad++;
         rhp_req_t r;
@@ -164,6 +169,22 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
     stats[1] = st_count.fast_bad;
     stats[2] = st_count.exact;
   }
+  return 0;
+}
+
+/* rhp_fixup_sessions (rhp.h) on the host: the same walk (rhp_scalar.h
+ * fixup_session_t) over a speculative batch parsed by rhp_cpu_parse_batch or
+ * rhp_emu_parse_batch. */
+extern "C" int rhp_cpu_fixup_sessions(const rhp_batch_t *b, const rhp_session_t *sessions, uint32_t n_sessions,
+                                      rhp_session_result_t *results, uint64_t *req_start)
+{
+  if (!b || b->mode != RHP_MODE_HTTP || !(b->flags & RHP_BATCH_SPECULATIVE)) return -22;
+  const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR;
+  const FixupIO io{b->bytes_rw, b->offsets, b->reqs, b->hdrs, b->http, hmajor ? 1u : b->max_headers,
+                   hmajor ? (uint64_t) b->n : 1u, b->max_headers};
+  for (uint32_t k = 0; k < n_sessions; k++)
+    fixup_session_t(io, sessions[k].piece_lo, sessions[k].piece_hi, req_start, &results[k],
+                    [&](uint64_t at) { return PlainBytes{b->bytes_rw + at}; });
   return 0;
 }
 

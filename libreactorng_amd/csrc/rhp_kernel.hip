@@ -55,6 +55,7 @@ struct Params {
   rhp_hdr_t *hdrs;
   rhp_http_t *http;
   const uint64_t *last_len;   /* phr mode, may be NULL: is_complete first where != 0 */
+  bool compact;               /* http mode: de-frame chunked bodies in place (not speculative) */
   uint32_t n;
   uint32_t max_headers;
   uint32_t mode;
@@ -175,7 +176,7 @@ __device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64
   if (p.mode == RHP_MODE_HTTP) {
     rhp_http_t x;
     LineBytes B{p.bytes_rw + off, ~0ull, {0, 0, 0, 0}};
-    scalar_http_t(B, p.bytes_rw + off, len, p.max_headers, &r, h, p.hs_hdr, &x);
+    scalar_http_t(B, p.bytes_rw + off, len, p.max_headers, &r, h, p.hs_hdr, &x, p.compact);
     p.http[i] = x;
   } else {
     LineBytes B{p.bytes + off, ~0ull, {0, 0, 0, 0}};
@@ -1282,7 +1283,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       } else {
         const uint32_t cand = h.hint[0];
         http_frame(p.bytes_rw + h.off, h.end - h.off, p.reqs[i], p.hdrs + (uint64_t) i * p.hs_req, p.hs_hdr,
-                   &p.http[i], (cand >> 31) ? ~0ull : (uint64_t) (cand & 0x3fffffffu));
+                   &p.http[i], (cand >> 31) ? ~0ull : (uint64_t) (cand & 0x3fffffffu), p.compact);
       }
     };
     uint32_t *slow = reinterpret_cast<uint32_t *>(lds + kLdsTable);   /* the staging area, idle now */
@@ -1347,6 +1348,18 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     for (int k = 0; k < 4; k++) g_stamps[w * kStampSlots + 15 + k] = rp[k];
   }
 #endif
+}
+
+/* rhp_fixup_sessions: one thread per session (rhp_scalar.h fixup_session_t) */
+__global__ __launch_bounds__(256) void rhp_fixup_kernel(Params p, const rhp_session_t *sessions, uint32_t n_sessions,
+                                                       rhp_session_result_t *results, uint64_t *req_start)
+{
+  const FixupIO io{p.bytes_rw, p.offsets, p.reqs, p.hdrs, p.http, p.hs_req, p.hs_hdr, p.max_headers};
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_sessions; k += gridDim.x * blockDim.x) {
+    const rhp_session_t ss = sessions[k];
+    fixup_session_t(io, ss.piece_lo, ss.piece_hi, req_start, &results[k],
+                    [&](uint64_t at) { return LineBytes{p.bytes_rw + at, ~0ull, {0, 0, 0, 0}}; });
+  }
 }
 
 /* Exact-path-only kernel: one request per thread, grid-stride (RHP_IMPL_EXACT). */
@@ -1450,6 +1463,7 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   if (b->mode != RHP_MODE_PHR && b->mode != RHP_MODE_HTTP) return -22;
   if (b->layout != RHP_LAYOUT_REQUEST_MAJOR && b->layout != RHP_LAYOUT_HEADER_MAJOR) return -22;
   if (b->last_len && b->mode != RHP_MODE_PHR) return -22;   /* http_read_request passes last_len 0 */
+  if ((b->flags & ~RHP_BATCH_SPECULATIVE) || ((b->flags & RHP_BATCH_SPECULATIVE) && b->mode != RHP_MODE_HTTP)) return -22;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int dev = 0, cus = 0;
   {
@@ -1468,6 +1482,7 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.hdrs = b->hdrs;
   prm.http = b->http;
   prm.last_len = b->last_len;
+  prm.compact = !(b->flags & RHP_BATCH_SPECULATIVE);
   prm.n = b->n;
   prm.max_headers = b->max_headers;
   prm.mode = b->mode;
@@ -1488,6 +1503,34 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   if (b->mode == RHP_MODE_HTTP) return launch_dfa<16, true, true>(prm, s, dev, cus);
   if (late) return launch_dfa<16, true, false>(prm, s, dev, cus);
   return launch_dfa<16, false, false>(prm, s, dev, cus);
+}
+
+int rhp_fixup_sessions(const rhp_batch_t *b, const rhp_session_t *sessions, uint32_t n_sessions,
+                       rhp_session_result_t *results, uint64_t *req_start, void *stream)
+{
+  if (!b || (n_sessions && (!sessions || !results || !req_start))) return -22;
+  if (n_sessions == 0) return 0;
+  if (b->mode != RHP_MODE_HTTP || !(b->flags & RHP_BATCH_SPECULATIVE)) return -22;
+  if (!b->bytes_rw || !b->offsets || !b->reqs || !b->http || (b->max_headers && !b->hdrs)) return -22;
+  if (b->layout != RHP_LAYOUT_REQUEST_MAJOR && b->layout != RHP_LAYOUT_HEADER_MAJOR) return -22;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  Params prm = {};
+  prm.bytes = b->bytes;
+  prm.bytes_rw = b->bytes_rw;
+  prm.offsets = b->offsets;
+  prm.reqs = b->reqs;
+  prm.hdrs = b->hdrs;
+  prm.http = b->http;
+  prm.n = b->n;
+  prm.max_headers = b->max_headers;
+  prm.mode = b->mode;
+  prm.compact = true;
+  const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR;
+  prm.hs_req = hmajor ? 1u : b->max_headers;
+  prm.hs_hdr = hmajor ? b->n : 1u;
+  const uint32_t grid = (n_sessions + 255u) / 256u;
+  hipLaunchKernelGGL(rhp_fixup_kernel, dim3(grid), dim3(256), 0, s, prm, sessions, n_sessions, results, req_start);
+  return (int) hipGetLastError();
 }
 
 }  // extern "C"

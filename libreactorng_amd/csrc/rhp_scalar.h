@@ -332,15 +332,22 @@ RHP_HD int64_t one_chunk(const uint8_t *in, uint64_t size, uint64_t *data_off, u
   return (int64_t) (cs + n + 2);
 }
 
-/* http_dechunk (http.c:134-160): validate, then compact payloads in place */
-RHP_HD int64_t dechunk(uint8_t *in, uint64_t size, uint64_t *body_len)
+/* http_dechunk (http.c:134-160): validate, then compact payloads in place.
+ * compact = false (speculative batches, rhp.h RHP_BATCH_SPECULATIVE): validate
+ * only and report the payload length; nothing is written */
+RHP_HD int64_t dechunk(uint8_t *in, uint64_t size, uint64_t *body_len, bool compact = true)
 {
-  uint64_t off = 0, doff = 0, dlen = 0;
+  uint64_t off = 0, doff = 0, dlen = 0, sum = 0;
   do {
     int64_t n = one_chunk(in + off, size - off, &doff, &dlen);
     if (n <= 0) return n;
     off += (uint64_t) n;
+    sum += dlen;
   } while (dlen);
+  if (!compact) {
+    *body_len = sum;
+    return (int64_t) off;
+  }
   uint64_t total = 0;
   off = 0;
   do {
@@ -361,7 +368,7 @@ RHP_HD int64_t dechunk(uint8_t *in, uint64_t size, uint64_t *body_len)
  * checks every header */
 template <class HV>
 RHP_HD void http_frame_t(uint8_t *b, uint64_t len, int64_t n, bool get, const HV &hv, uint32_t nh, rhp_http_t *x,
-                         uint64_t cand = ~0ull)
+                         uint64_t cand = ~0ull, bool compact = true)
 {
   /* one framing candidate (the common case): its name is read together with
    * its value digits, so the GPU replay makes fewer memory round trips */
@@ -402,17 +409,18 @@ RHP_HD void http_frame_t(uint8_t *b, uint64_t len, int64_t n, bool get, const HV
     for (uint32_t i = 0; eq && i < 7; i++) eq = upper(v[i]) == (uint32_t) ch[i];
     if (!eq) { x->result = -1; x->consumed = 0; return; }
     uint64_t blen = 0;
-    int64_t size = dechunk(b + n, len - (uint64_t) n, &blen);
+    int64_t size = dechunk(b + n, len - (uint64_t) n, &blen, compact);
     if (size <= 0) { x->result = (int32_t) size; x->consumed = 0; return; }
-    x->body_kind = 1; x->body_len = blen; x->consumed = (uint64_t) n + (uint64_t) size;
+    x->body_kind = compact ? 1u : RHP_BODY_CHUNKED_PENDING;
+    x->body_len = blen; x->consumed = (uint64_t) n + (uint64_t) size;
   }
 }
 
 RHP_HD void http_frame(uint8_t *b, uint64_t len, const rhp_req_t &r, const rhp_hdr_t *h, uint64_t hs, rhp_http_t *x,
-                       uint64_t cand = ~0ull)
+                       uint64_t cand = ~0ull, bool compact = true)
 {
   const bool get = r.method_len == 3 && ((b[r.method_off] == 'G') & (b[r.method_off + 1] == 'E') & (b[r.method_off + 2] == 'T'));
-  http_frame_t(b, len, r.ret, get, HdrsRec{b, h, hs}, r.num_headers, x, cand);
+  http_frame_t(b, len, r.ret, get, HdrsRec{b, h, hs}, r.num_headers, x, cand, compact);
 }
 
 /* phr status -> http_read_request result when the parse gave no request
@@ -423,18 +431,84 @@ RHP_HD int32_t http_result_of(int n) { return n == kBad ? -1 : n == RHP_RET_TOOL
 /* Whole http_read_request for one request. */
 template <class Bytes>
 RHP_HD void scalar_http_t(Bytes &B, uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, uint64_t hs,
-                          rhp_http_t *x)
+                          rhp_http_t *x, bool compact = true)
 {
   int n = scalar_phr_t(B, len, max, r, h, hs);
   x->body_kind = 0; x->consumed = 0; x->body_len = 0;
   if (len == 0) { x->result = 0; return; }
   if (n <= 0) { x->result = http_result_of(n); return; }
-  http_frame(b, len, *r, h, hs, x);
+  http_frame(b, len, *r, h, hs, x, ~0ull, compact);
 }
 RHP_HD void scalar_http(uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, uint64_t hs, rhp_http_t *x)
 {
   PlainBytes B{b};
   scalar_http_t(B, b, len, max, r, h, hs, x);
+}
+
+/* rhp_fixup_sessions (rhp.h) for one session: the pieces' speculative
+ * results are taken where they are what http_read_request over the rest of
+ * the input would return, and the rest is parsed again from the true request
+ * boundaries; `mk(at)` gives a byte reader for the batch bytes at `at`.  The
+ * loop is the reference's server_session_read (server.c:37-65): one
+ * http_read_request per request, advancing by what it consumed. */
+struct FixupIO {
+  uint8_t *bytes_rw;
+  const uint64_t *off;
+  rhp_req_t *reqs;
+  rhp_hdr_t *hdrs;
+  rhp_http_t *http;
+  uint64_t hs_req, hs_hdr;   /* record k of request i at hdrs[i * hs_req + k * hs_hdr] */
+  uint32_t max_headers;
+};
+
+template <class MakeBytes>
+RHP_HD void fixup_session_t(const FixupIO &io, uint32_t p_lo, uint32_t p_hi, uint64_t *req_start,
+                            rhp_session_result_t *out, MakeBytes mk)
+{
+  const uint64_t b_lo = io.off[p_lo], b_hi = io.off[p_hi];
+  uint64_t pos = b_lo;
+  uint32_t slot = p_lo, j = p_lo, more = 0;
+  while (pos < b_hi) {
+    if (slot == p_hi) { more = 1; break; }
+    while (j < p_hi && io.off[j] < pos) j++;
+    rhp_http_t x;
+    bool taken = false;
+    if (j < p_hi && io.off[j] == pos) {
+      x = io.http[j];
+      const uint64_t plen = io.off[j + 1] - pos;
+      taken = (x.result == 1 && x.consumed <= plen) || x.result == -1 || x.result == RHP_RET_TOOLONG ||
+              (x.result == 0 && j + 1 == p_hi);
+    }
+    if (taken) {
+      const rhp_req_t r = io.reqs[j];
+      if (x.result == 1 && x.body_kind == RHP_BODY_CHUNKED_PENDING) {
+        /* a true request boundary now: de-frame its chunked body in place
+         * (http.c:225-229, the memmove of http_dechunk) */
+        uint64_t blen = 0;
+        (void) dechunk(io.bytes_rw + pos + (uint64_t) r.ret, x.consumed - (uint64_t) r.ret, &blen, true);
+        x.body_kind = 1;
+      }
+      if (j != slot) {
+        io.reqs[slot] = r;
+        const uint32_t nh = r.ret > 0 ? r.num_headers : 0u;
+        for (uint32_t k = 0; k < nh; k++)
+          io.hdrs[(uint64_t) slot * io.hs_req + k * io.hs_hdr] = io.hdrs[(uint64_t) j * io.hs_req + k * io.hs_hdr];
+      }
+      io.http[slot] = x;
+    } else {
+      auto B = mk(pos);
+      scalar_http_t(B, io.bytes_rw + pos, b_hi - pos, io.max_headers, &io.reqs[slot],
+                    io.hdrs + (uint64_t) slot * io.hs_req, io.hs_hdr, &x, true);
+      io.http[slot] = x;
+    }
+    req_start[slot] = pos;
+    slot++;
+    if (x.result != 1) break;
+    pos += x.consumed;
+  }
+  out->n_slots = slot - p_lo;
+  out->more = more;
+  out->consumed = pos - b_lo;
 }
 
 }  // namespace rhp

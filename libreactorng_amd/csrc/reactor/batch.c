@@ -43,10 +43,17 @@
 
 enum { PARSER_UNSET, PARSER_GPU, PARSER_HOST, PARSER_HOST_ASYNC };
 
+/* A slot's round lives in ONE buffer, the same layout on the host (pinned) and
+ * the device: the input [bytes + RHP_PAD | offsets | sessions] goes over in one
+ * H2D copy, the records and the (de-framed) bytes come back in one D2H copy:
+ * [bytes | offsets | sessions | reqs | hdrs | http | req_start | session results] */
 typedef struct slot
 {
-  size_t       cap_bytes, cap_n;
-  uint8_t     *h_bytes;      /* pinned (gpu) or malloc'd (host) staging */
+  size_t       cap;          /* bytes of h_buf / d_buf */
+  uint8_t     *h_buf, *d_buf;
+  size_t       in_size, out_size;   /* this round: the input prefix, the whole layout */
+  size_t       o_off, o_sess, o_req, o_hdr, o_http, o_start, o_sres;
+  uint8_t     *h_bytes;      /* = h_buf */
   uint64_t    *h_off;
   rhp_req_t   *h_req;
   rhp_hdr_t   *h_hdr;
@@ -54,8 +61,6 @@ typedef struct slot
   uint64_t    *h_start;      /* rhp_fixup_sessions: where each record slot's request starts */
   rhp_session_t        *h_sess;
   rhp_session_result_t *h_sres;
-  size_t       cap_sess;
-  void        *d_bytes, *d_off, *d_req, *d_hdr, *d_http, *d_start, *d_sess, *d_sres;
   uint32_t     n, n_sess;
   size_t       bytes;
   uint64_t     t_submit;
@@ -73,7 +78,15 @@ typedef struct batch_state
   int          stats;
   int          diag_host;   /* RHP_REACTOR_DIAG=hostparse: gpu-mode buffers, host parse (diagnostic) */
   uint64_t     st_rounds, st_requests, st_ns;
-  /* host-async: the worker's queue of submitted slots (in order) */
+  /* gpu: how a round's completion reaches the eventfd (RHP_REACTOR_COMPLETE):
+   * COMPLETE_HOSTFUNC a hipLaunchHostFunc behind the round's copies (the HIP
+   * runtime's callback thread writes the eventfd); COMPLETE_EVENT a waiter
+   * thread of ours blocks in hipEventSynchronize on the round's event
+   * (hipEventBlockingSync) and writes it; COMPLETE_SPIN the waiter polls
+   * hipEventQuery (lowest latency, one busy core while rounds are in flight) */
+  int             complete;
+  hipEvent_t      ev[REACTOR_BATCH_SLOTS];
+  /* host-async, and the gpu waiter: the worker's queue of submitted slots (in order) */
   pthread_t       worker;
   pthread_mutex_t mu;
   pthread_cond_t  cv;
@@ -104,6 +117,40 @@ static void *host_worker(void *arg)
     host_parse(b, k);
     /* the entry leaves the queue before the loop thread hears of the round:
      * it may finish the slot and submit it again right after the write */
+    pthread_mutex_lock(&b->mu);
+    b->q_head = (b->q_head + 1) % REACTOR_BATCH_SLOTS;
+    b->q_n--;
+    pthread_cond_broadcast(&b->cv);
+    pthread_mutex_unlock(&b->mu);
+    const uint64_t one = 1;
+    ssize_t r = write(b->efd, &one, sizeof one);
+    (void) r;
+    pthread_mutex_lock(&b->mu);
+  }
+  return NULL;
+}
+
+enum { COMPLETE_HOSTFUNC, COMPLETE_EVENT, COMPLETE_SPIN };
+
+/* gpu completion waiter (COMPLETE_EVENT / COMPLETE_SPIN): the state is its
+ * creator's (B is per thread) */
+static void *gpu_waiter(void *arg)
+{
+  batch_state_t *b = arg;
+  pthread_mutex_lock(&b->mu);
+  for (;;)
+  {
+    while (!b->q_n)
+      pthread_cond_wait(&b->cv, &b->mu);
+    const int k = b->q[b->q_head];
+    pthread_mutex_unlock(&b->mu);
+    if (b->complete == COMPLETE_SPIN)
+    {
+      while (hipEventQuery(b->ev[k]) == hipErrorNotReady)
+        ;
+    }
+    else
+      (void) hipEventSynchronize(b->ev[k]);
     pthread_mutex_lock(&b->mu);
     b->q_head = (b->q_head + 1) % REACTOR_BATCH_SLOTS;
     b->q_n--;
@@ -161,6 +208,14 @@ static int parser(void)
       if (n < 1)
         die("hipGetDeviceCount", 0);
       HIP(hipStreamCreateWithFlags(&B.stream, hipStreamNonBlocking));
+      const char *c = getenv("RHP_REACTOR_COMPLETE");
+      B.complete = !c ? COMPLETE_EVENT : strcmp(c, "hostfunc") == 0 ? COMPLETE_HOSTFUNC
+                                       : strcmp(c, "spin") == 0   ? COMPLETE_SPIN
+                                                                  : COMPLETE_EVENT;
+      if (B.complete != COMPLETE_HOSTFUNC)
+        for (int k = 0; k < REACTOR_BATCH_SLOTS; k++)
+          HIP(hipEventCreateWithFlags(&B.ev[k], hipEventDisableTiming |
+                                                    (B.complete == COMPLETE_EVENT ? hipEventBlockingSync : 0)));
     }
     if (B.parser != PARSER_HOST)
     {
@@ -168,11 +223,11 @@ static int parser(void)
       if (B.efd < 0)
         die("eventfd", errno);
     }
-    if (B.parser == PARSER_HOST_ASYNC)
+    if (B.parser == PARSER_HOST_ASYNC || (B.parser == PARSER_GPU && B.complete != COMPLETE_HOSTFUNC))
     {
       pthread_mutex_init(&B.mu, NULL);
       pthread_cond_init(&B.cv, NULL);
-      if (pthread_create(&B.worker, NULL, host_worker, &B) != 0)
+      if (pthread_create(&B.worker, NULL, B.parser == PARSER_GPU ? gpu_waiter : host_worker, &B) != 0)
         abort();
       pthread_detach(B.worker);
     }
@@ -224,80 +279,50 @@ static void dev_free(void **p)
   *p = NULL;
 }
 
+static size_t up16(size_t x) { return (x + 15u) & ~(size_t) 15u; }
+
 uint8_t *reactor_batch_reserve(int k, size_t bytes, uint32_t n, uint32_t n_sessions)
 {
   (void) parser();
   slot_t *s = &B.slot[k];
-  if (n_sessions > s->cap_sess)
-  {
-    size_t c = s->cap_sess ? s->cap_sess : 1024;
-    while (c < n_sessions)
-      c *= 2;
-    host_free(s->h_sess);
-    host_free(s->h_sres);
-    s->h_sess = host_alloc(c * sizeof *s->h_sess);
-    s->h_sres = host_alloc(c * sizeof *s->h_sres);
-    if (B.parser == PARSER_GPU)
-    {
-      dev_free(&s->d_sess);
-      dev_free(&s->d_sres);
-      HIP(hipMalloc(&s->d_sess, c * sizeof *s->h_sess));
-      HIP(hipMalloc(&s->d_sres, c * sizeof *s->h_sres));
-    }
-    s->cap_sess = c;
-  }
-  const size_t need = bytes + RHP_PAD;
-  if (need > s->cap_bytes)
+  s->o_off = up16(bytes + RHP_PAD);
+  s->o_sess = s->o_off + up16((n + 1u) * sizeof(uint64_t));
+  s->in_size = s->o_sess + up16(n_sessions * sizeof(rhp_session_t));
+  s->o_req = s->in_size;
+  s->o_hdr = s->o_req + up16(n * sizeof(rhp_req_t));
+  s->o_http = s->o_hdr + up16((size_t) n * REACTOR_BATCH_HEADERS * sizeof(rhp_hdr_t));
+  s->o_start = s->o_http + up16(n * sizeof(rhp_http_t));
+  s->o_sres = s->o_start + up16(n * sizeof(uint64_t));
+  s->out_size = s->o_sres + up16(n_sessions * sizeof(rhp_session_result_t));
+  if (s->out_size > s->cap)
   {
     /* generous first capacities: growing pinned and device buffers costs
      * milliseconds per step (page pinning, frees that synchronise) */
-    size_t c = s->cap_bytes ? s->cap_bytes : 1u << 20;
-    while (c < need)
+    size_t c = s->cap ? s->cap : 4u << 20;
+    while (c < s->out_size)
       c *= 2;
-    host_free(s->h_bytes);
-    s->h_bytes = host_alloc(c);
+    host_free(s->h_buf);
+    s->h_buf = host_alloc(c);
     if (B.parser == PARSER_GPU)
     {
-      dev_free(&s->d_bytes);
-      HIP(hipMalloc(&s->d_bytes, c));
-    }
-    s->cap_bytes = c;
-  }
-  if (n + 1 > s->cap_n)
-  {
-    size_t c = s->cap_n ? s->cap_n : 4096;
-    while (c < n + 1u)
-      c *= 2;
-    host_free(s->h_off);
-    host_free(s->h_req);
-    host_free(s->h_hdr);
-    host_free(s->h_http);
-    host_free(s->h_start);
-    s->h_start = host_alloc(c * sizeof *s->h_start);
-    s->h_off = host_alloc(c * sizeof *s->h_off);
-    s->h_req = host_alloc(c * sizeof *s->h_req);
-    s->h_hdr = host_alloc(c * REACTOR_BATCH_HEADERS * sizeof *s->h_hdr);
-    s->h_http = host_alloc(c * sizeof *s->h_http);
-    if (B.parser == PARSER_GPU)
-    {
-      dev_free(&s->d_off);
-      dev_free(&s->d_req);
-      dev_free(&s->d_hdr);
-      dev_free(&s->d_http);
-      dev_free(&s->d_start);
-      HIP(hipMalloc(&s->d_start, c * sizeof *s->h_start));
-      HIP(hipMalloc(&s->d_off, c * sizeof *s->h_off));
-      HIP(hipMalloc(&s->d_req, c * sizeof *s->h_req));
-      HIP(hipMalloc(&s->d_hdr, c * REACTOR_BATCH_HEADERS * sizeof *s->h_hdr));
-      HIP(hipMalloc(&s->d_http, c * sizeof *s->h_http));
+      dev_free((void **) &s->d_buf);
+      HIP(hipMalloc((void **) &s->d_buf, c));
       if (!B.d_work)
       {
         HIP(hipMalloc(&B.d_work, RHP_WORK_WORDS * sizeof(uint32_t)));
         HIP(hipMemsetAsync(B.d_work, 0, RHP_WORK_WORDS * sizeof(uint32_t), B.stream));
       }
     }
-    s->cap_n = c;
+    s->cap = c;
   }
+  s->h_bytes = s->h_buf;
+  s->h_off = (uint64_t *) (s->h_buf + s->o_off);
+  s->h_sess = (rhp_session_t *) (s->h_buf + s->o_sess);
+  s->h_req = (rhp_req_t *) (s->h_buf + s->o_req);
+  s->h_hdr = (rhp_hdr_t *) (s->h_buf + s->o_hdr);
+  s->h_http = (rhp_http_t *) (s->h_buf + s->o_http);
+  s->h_start = (uint64_t *) (s->h_buf + s->o_start);
+  s->h_sres = (rhp_session_result_t *) (s->h_buf + s->o_sres);
   return s->h_bytes;
 }
 
@@ -358,32 +383,39 @@ void reactor_batch_submit(int k, uint32_t n, size_t bytes, uint32_t n_sessions)
       round_done((void *) (intptr_t) B.efd);   /* diagnostic mode keeps the asynchronous protocol */
     return;
   }
-  HIP(hipMemcpyAsync(s->d_bytes, s->h_bytes, bytes + RHP_PAD, hipMemcpyHostToDevice, B.stream));
-  HIP(hipMemcpyAsync(s->d_off, s->h_off, (n + 1) * sizeof *s->h_off, hipMemcpyHostToDevice, B.stream));
-  HIP(hipMemcpyAsync(s->d_sess, s->h_sess, n_sessions * sizeof *s->h_sess, hipMemcpyHostToDevice, B.stream));
+  HIP(hipMemcpyAsync(s->d_buf, s->h_buf, s->in_size, hipMemcpyHostToDevice, B.stream));   /* bytes, offsets, sessions */
   /* the pieces speculatively, then every session walked in order from its
    * true request boundaries (include/rhp.h rhp_fixup_sessions): all of a
    * round's pipelined requests, bodies included, in this one round */
+  uint8_t *d = s->d_buf;
   rhp_batch_t b = {
-    .bytes = s->d_bytes, .bytes_rw = s->d_bytes, .offsets = s->d_off, .bytes_size = bytes + RHP_PAD, .n = n,
-    .max_headers = REACTOR_BATCH_HEADERS, .mode = RHP_MODE_HTTP, .reqs = s->d_req, .hdrs = s->d_hdr, .http = s->d_http,
-    .work = B.d_work, .flags = RHP_BATCH_SPECULATIVE};
+    .bytes = d, .bytes_rw = d, .offsets = (const uint64_t *) (d + s->o_off), .bytes_size = bytes + RHP_PAD, .n = n,
+    .max_headers = REACTOR_BATCH_HEADERS, .mode = RHP_MODE_HTTP, .reqs = (rhp_req_t *) (d + s->o_req),
+    .hdrs = (rhp_hdr_t *) (d + s->o_hdr), .http = (rhp_http_t *) (d + s->o_http), .work = B.d_work,
+    .flags = RHP_BATCH_SPECULATIVE};
   int rc = rhp_parse_batch(&b, B.stream);
   if (rc != 0)
     die("rhp_parse_batch", rc);
-  rc = rhp_fixup_sessions(&b, s->d_sess, n_sessions, s->d_sres, s->d_start, B.stream);
+  rc = rhp_fixup_sessions(&b, (const rhp_session_t *) (d + s->o_sess), n_sessions,
+                          (rhp_session_result_t *) (d + s->o_sres), (uint64_t *) (d + s->o_start), B.stream);
   if (rc != 0)
     die("rhp_fixup_sessions", rc);
-  HIP(hipMemcpyAsync(s->h_req, s->d_req, n * sizeof *s->h_req, hipMemcpyDeviceToHost, B.stream));
-  HIP(hipMemcpyAsync(s->h_hdr, s->d_hdr, (size_t) n * REACTOR_BATCH_HEADERS * sizeof *s->h_hdr, hipMemcpyDeviceToHost,
-                     B.stream));
-  HIP(hipMemcpyAsync(s->h_http, s->d_http, n * sizeof *s->h_http, hipMemcpyDeviceToHost, B.stream));
-  HIP(hipMemcpyAsync(s->h_sres, s->d_sres, n_sessions * sizeof *s->h_sres, hipMemcpyDeviceToHost, B.stream));
-  HIP(hipMemcpyAsync(s->h_start, s->d_start, n * sizeof *s->h_start, hipMemcpyDeviceToHost, B.stream));
-  /* chunked bodies are de-framed in place (http.c:155) by the fix-up: the
-   * round's bytes come back with the records, one asynchronous copy */
-  HIP(hipMemcpyAsync(s->h_bytes, s->d_bytes, bytes, hipMemcpyDeviceToHost, B.stream));
-  HIP(hipLaunchHostFunc(B.stream, round_done, (void *) (intptr_t) B.efd));
+  /* the records, and the bytes (chunked bodies are de-framed in place by the
+   * fix-up, http.c:155): one asynchronous copy of the whole layout */
+  HIP(hipMemcpyAsync(s->h_buf, s->d_buf, s->out_size, hipMemcpyDeviceToHost, B.stream));
+  if (B.complete == COMPLETE_HOSTFUNC)
+  {
+    HIP(hipLaunchHostFunc(B.stream, round_done, (void *) (intptr_t) B.efd));
+    return;
+  }
+  HIP(hipEventRecord(B.ev[k], B.stream));
+  pthread_mutex_lock(&B.mu);
+  if (B.q_n >= REACTOR_BATCH_SLOTS)
+    die("reactor_batch_submit: queue full", B.q_n);
+  B.q[(B.q_head + B.q_n) % REACTOR_BATCH_SLOTS] = k;
+  B.q_n++;
+  pthread_cond_broadcast(&B.cv);
+  pthread_mutex_unlock(&B.mu);
 }
 
 int reactor_batch_completed(void)
@@ -398,7 +430,7 @@ void reactor_batch_wait(void)
 {
   if (B.parser == PARSER_GPU)
     HIP(hipStreamSynchronize(B.stream));
-  if (B.parser == PARSER_HOST_ASYNC)
+  if (B.parser == PARSER_HOST_ASYNC || (B.parser == PARSER_GPU && B.complete != COMPLETE_HOSTFUNC))
   {
     pthread_mutex_lock(&B.mu);
     while (B.q_n)

@@ -109,11 +109,11 @@ def test_burst_rounds_gpu_vs_host():
           f"host {host:.0f} ({host_round:.0f})")
     print(out_g, out_w, out_h)
     assert gpu_round >= 4000 and host_round >= 4000
-    # a guard against a pathological regression only: the medians of 8 bursts
-    # vary between boxes with the host side of a round (one box measured the GPU
-    # rounds at 0.39x the host parser, 2.2 ms from submit to the eventfd, where
-    # others measure 1.0-1.05x)
-    assert gpu >= 0.25 * host, (gpu, host)
+    # round completion by our own waiter thread blocked on the round's event
+    # (RHP_REACTOR_COMPLETE=event, the default) rather than the HIP runtime's
+    # host-function thread: 2.17 M req/s against the host parser's 2.19 M
+    # (profiles/r03/reactor/); the parse is ~10 % of a burst's time
+    assert gpu >= 0.8 * host, (gpu, host)
 
 
 @pytest.mark.gpu

@@ -73,13 +73,20 @@ def shard_range(n_total: int, rank: int, world: int):
 def traffic_from_profile(config_key: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of this
     kernel (profiles/pmc_traffic.json: FETCH_SIZE x 2 on gfx950 + WRITE_SIZE),
-    with the profile it came from; (None, None) if absent."""
+    the profile it came from, and whether that profile was taken on the library
+    this run loads (its sha256); (None, None, False) if absent."""
+    import hashlib
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path)).get(config_key, {})
-        return d.get("hbm_bytes_per_launch"), d.get("source")
+        lib = os.environ.get("RHP_LIB", os.path.join(ROOT, "libreactorng_amd", "librhp.so"))
+        match = d.get("library_sha256") == hashlib.sha256(open(lib, "rb").read()).hexdigest()
+        if not match:
+            print(f"bench.py: profiles/pmc_traffic.json ({config_key}) was not measured on the library this run "
+                  f"loads: roofline.traffic is stale", file=sys.stderr)
+        return d.get("hbm_bytes_per_launch"), d.get("source"), match
     except Exception:
-        return None, None
+        return None, None, False
 
 
 def cpu_info():
@@ -344,9 +351,10 @@ def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
 
 def roofline(r, key):
     achieved = r["alg_bytes"] / (r["kern_ms"] * 1e-3) / 1e9
-    traffic, source = traffic_from_profile(key)
+    traffic, source, match = traffic_from_profile(key)
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": source,
+            "traffic_library_match": match,
             "kernel_ms": round(r["kern_ms"], 4), "algorithmic_bytes_per_launch": int(r["alg_bytes"])}
 
 
@@ -362,6 +370,7 @@ def main(argv=None):
     ap.add_argument("--copies", type=int, default=4)
     ap.add_argument("--per-gpu", type=int, default=0, help="requests per GPU (default: the config's 1M)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end leg")
     ap.add_argument("--impl", type=int, default=rhp.IMPL_DFA)
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--layout", default="auto", choices=["auto"] + sorted(LAYOUTS),
@@ -420,6 +429,13 @@ def main(argv=None):
         }
         if extra:
             line["extra_configs"] = extra
+        if world == 1 and args.device == "gpu" and not args.no_e2e:
+            # north_star: the path starts and ends in host memory; the rate with
+            # pinned H2D -> kernel -> D2H of the records, chunked over 3 streams
+            # (never `value`, which is device-resident)
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            from e2e_pcie import e2e
+            line["e2e"] = e2e(args.config, per_gpu, reps=3)
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline([args.config] + [k for k in ("zipf", "post") if k in extra])
         print(json.dumps(line), flush=True)

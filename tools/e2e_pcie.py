@@ -27,14 +27,9 @@ import libreactorng_amd as rhp  # noqa: E402
 from bench import CONFIGS  # noqa: E402
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="get256", choices=sorted(CONFIGS))
-    ap.add_argument("--n", type=int, default=1 << 20)
-    ap.add_argument("--chunks", type=int, default=16)
-    ap.add_argument("--streams", type=int, default=3)
-    ap.add_argument("--reps", type=int, default=5)
-    args = ap.parse_args()
+def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
+    """The end-to-end measurement as a dict (bench.py's `e2e` object)."""
+    args = argparse.Namespace(config=config, n=n, chunks=chunks, streams=streams, reps=reps)
     cfg = CONFIGS[args.config]
     n, maxh, mode = args.n, cfg["maxh"], cfg["mode"]
     buf, off = rhp.generate(cfg["gen"], n, cfg["seed"])
@@ -99,7 +94,7 @@ def main():
     in_bytes = buf.size + off.nbytes
     out_bytes = h_reqs.numel() + h_hdrs.numel()
     gib = 2 ** 30
-    print(json.dumps({
+    return ({
         "config": args.config, "requests": n, "algorithmic_bytes": int(alg), "chunks": args.chunks,
         "streams": args.streams, "ok_fraction": ok_frac,
         "e2e_GiBps": round(alg / t_e2e / gib, 2), "e2e_ms": round(t_e2e * 1e3, 3),
@@ -107,7 +102,18 @@ def main():
         "h2d_GBps": round(in_bytes / t_h2d / 1e9, 2), "h2d_ms": round(t_h2d * 1e3, 3),
         "d2h_GBps": round(out_bytes / t_d2h / 1e9, 2), "d2h_ms": round(t_d2h * 1e3, 3),
         "h2d_bytes": int(in_bytes), "d2h_bytes": int(out_bytes),
-    }))
+    })
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="get256", choices=sorted(CONFIGS))
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--chunks", type=int, default=16)
+    ap.add_argument("--streams", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    print(json.dumps(e2e(a.config, a.n, a.chunks, a.streams, a.reps)))
 
 
 if __name__ == "__main__":

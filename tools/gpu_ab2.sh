@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT}" && mkdir -p gpurun_out && export TMPDIR=/tmp
 out=gpurun_out/ab_${TAG:-x}.txt; : > $out
 for r in $(seq 1 ${ROUNDS:-2}); do
   for l in $LIBS; do
-    RHP_LIB=$PWD/libreactorng_amd/librhp_x_${l%%@*}.so timeout -k 10 300 python bench.py ${BENCH_ARGS} $( [[ $l == *@* ]] && echo --layout ${l##*@} ) --no-cpu --steps 30 --warmup 5 --extra-steps 15 \
+    RHP_LIB=$PWD/libreactorng_amd/librhp_x_${l%%@*}.so timeout -k 10 300 python bench.py ${BENCH_ARGS} $( [[ $l == *@* ]] && echo --layout ${l##*@} ) --no-cpu --no-e2e --steps 30 --warmup 5 --extra-steps 15 \
       > gpurun_out/ab_$l.json 2>/dev/null || { echo "FAIL $l" >> $out; exit 1; }
     python - "$l" >> $out << 'PY'
 import json, sys

@@ -1,4 +1,6 @@
 mkdir -p gpurun_out
-timeout -k 10 120 ./tools/ubench_ceiling > gpurun_out/ceiling.txt 2>&1; cat gpurun_out/ceiling.txt
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "last_len or 4gib" > gpurun_out/pytest_lastlen.log 2>&1; tail -3 gpurun_out/pytest_lastlen.log
-LIBS="base prio8" ROUNDS=2 TAG=prio bash tools/gpu_ab2.sh
+for v in gpu:hostfunc gpu:event gpu:spin host:x gpu:event; do
+  p=${v%%:*}; c=${v##*:}
+  RHP_REACTOR_COMPLETE=$c RHP_REACTOR_PARSER=$p RHP_REACTOR_STATS=1 timeout -k 10 120 ./libreactorng_amd/bin/burst_test 64 64 9 > gpurun_out/burst_${p}_$c.txt 2>&1 || { cat gpurun_out/burst_${p}_$c.txt | tail; exit 1; }
+  echo "== $p $c"; grep -E "req/s" gpurun_out/burst_${p}_$c.txt | tail -9 | awk '{print $0}' | tr '\n' ' '; echo; grep -E "round" gpurun_out/burst_${p}_$c.txt | tail -3
+done

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-.}" && mkdir -p gpurun_out && export TMPDIR=/tmp
 TAG=${TAG:-pmcab}
 for l in ${LIBS}; do
   RHP_LIB=$PWD/libreactorng_amd/$l.so timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_BRANCH \
-    --output-format csv -d gpurun_out/${TAG}_$l -o p -- python3 bench.py --steps 4 --warmup 1 --no-cpu --copies 4 ${BENCH_ARGS} > gpurun_out/${TAG}_$l.log 2>&1 || exit 1
+    --output-format csv -d gpurun_out/${TAG}_$l -o p -- python3 bench.py --steps 4 --warmup 1 --no-cpu --no-e2e --copies 4 ${BENCH_ARGS} > gpurun_out/${TAG}_$l.log 2>&1 || exit 1
   python3 - "gpurun_out/${TAG}_$l" "$l" <<'PY'
 import csv, glob, sys, collections
 rows = []

@@ -7,7 +7,7 @@ timeout -k 10 120 rocprofv3 -L > gpurun_out/${TAG}_counters.txt 2>&1
 run() { # name counters...
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/${TAG}_$name -o p \
-    -- python3 bench.py --steps 6 --warmup 2 --no-cpu --copies 4 ${BENCH_ARGS} > gpurun_out/${TAG}_$name.log 2>&1
+    -- python3 bench.py --steps 6 --warmup 2 --no-cpu --no-e2e --copies 4 ${BENCH_ARGS} > gpurun_out/${TAG}_$name.log 2>&1
 }
 run sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
  && run sq2 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \

@@ -10,7 +10,7 @@ C=${CONFIG:-get256}
 run() { # name counters...
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/${TAG}_$name -o p \
-    -- python3 bench.py --config $C --extra none --steps 4 --warmup 1 --no-cpu ${BENCH_ARGS} > gpurun_out/${TAG}_$name.log 2>&1
+    -- python3 bench.py --config $C --extra none --steps 4 --warmup 1 --no-cpu --no-e2e ${BENCH_ARGS} > gpurun_out/${TAG}_$name.log 2>&1
 }
 run sqa SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS \
  && run sqb SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_WAVES \

@@ -47,6 +47,11 @@ def main():
                       "rhp_dfa_kernel dispatch; L2 fabric-side requests (Infinity Cache hits included)",
         }
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import hashlib
+    lib = os.path.join(root, "libreactorng_amd", "librhp.so")
+    sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    for v in res.values():
+        v["library_sha256"] = sha   # bench.py flags the numbers stale when the library it runs differs
     json.dump(res, open(os.path.join(root, "profiles", "pmc_traffic.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 

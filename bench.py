@@ -7,7 +7,8 @@ batch of synthetic requests already resident in HBM.
 
 Workloads:
   N=1  config 2: 1M x 256 B GET, 4 headers, max_headers 16 (phr mode) -> `value`;
-       configs 3 and 5 are timed too, in `extra_configs`
+       configs 3 and 5 and a chunked-body config are
+       timed too, in `extra_configs`
   N>1  config 4: config 2's generator sharded evenly, 1M requests per GPU
        (8M at N=8), no collective on the data path -> weak scaling
 
@@ -62,7 +63,16 @@ CONFIGS = {
     "post": dict(gen=rhp.GEN_POST1K, seed=0x5EED0005, maxh=16, mode=rhp.MODE_HTTP, per_gpu=1 << 20,
                  layout="header",
                  name="config5: 1M x 1 KiB POST, Content-Length body skip, 5% malformed (http_read_request)"),
+    # not a BASELINE config: the chunked body framing of http_read_request (http.c:73-160, 221-230),
+    # SURVEY.md §8f row 3; the bodies are de-framed in place, so every launch starts from restored bytes
+    "chunked": dict(gen=rhp.GEN_CHUNKED, seed=0x5EED0006, maxh=16, mode=rhp.MODE_HTTP, per_gpu=1 << 20,
+                    layout="header", rewrites=True,
+                    name="chunked: 1M x ~1 KiB POST, Transfer-Encoding: chunked (1-8 chunks), de-framed in place, "
+                         "5% malformed framing (http_read_request)"),
 }
+
+
+EXTRA_KEYS = ("zipf", "post", "chunked")   # timed beside config 2 at N=1 (extra_configs)
 
 
 def shard_range(n_total: int, rank: int, world: int):
@@ -138,7 +148,11 @@ def cpu_baseline(keys, seconds: float = 5.0, cold_bytes: int = 1 << 30):
         buf, off = rhp.generate(cfg["gen"], n, cfg["seed"])
         hb = rhp.header_bytes(cfg["gen"], n, cfg["seed"])
         ncopy = max(1, -(-cold_bytes // buf.nbytes))
+        rewrites = bool(cfg.get("rewrites"))
+        if rewrites:   # http_dechunk rewrites the bytes: a pass parses a copy restored two passes earlier
+            ncopy = max(3, ncopy)
         bufs = [buf] + [buf.copy() for _ in range(ncopy - 1)]
+        pristine = buf.copy() if rewrites else None
         chk = ctypes.c_long(0)
         if have_ref:
             fn = ref.ref_http_batch_mt if cfg["mode"] == rhp.MODE_HTTP else ref.ref_phr_batch_mt
@@ -169,8 +183,13 @@ def cpu_baseline(keys, seconds: float = 5.0, cold_bytes: int = 1 << 30):
             if kind == "port" and cfg["mode"] == rhp.MODE_HTTP and t > 1:
                 continue
             run(bufs[-1], t)   # warm-up pass (threads, page tables), then rotate from the copy touched longest ago
+            if rewrites:
+                for b in bufs[:2]:
+                    np.copyto(b, pristine)
             ns, passes = 0, 0
             while passes < 2 or ns < seconds / 2 * 1e9:
+                if rewrites:   # untimed: the timed span is inside run()
+                    np.copyto(bufs[(passes + 2) % ncopy], pristine)
                 ns += run(bufs[passes % ncopy], t)
                 passes += 1
             res[t] = (hb * passes / (ns / 1e9) / 2 ** 30, passes)
@@ -228,7 +247,14 @@ class GpuRunner:
         import torch
         self.torch = torch
         buf, off = rhp.generate(cfg["gen"], hi - lo, cfg["seed"], lo=lo)
+        # a config whose launches rewrite the bytes (chunked bodies, http.c:155) restores a copy from
+        # this pristine one before it is launched again: >= 3 copies, restored two launches ahead
+        self.rewrites = bool(cfg.get("rewrites"))
+        if self.rewrites:
+            copies = max(3, copies)
         self.copies = [rhp.DeviceBatch(buf, off, cfg["maxh"], cfg["mode"], layout=layout) for _ in range(max(1, copies))]
+        self.pristine = self.copies[0].bytes.clone() if self.rewrites else None
+        self.nstep = 0
         # one set of output records per stream (batches in flight at once never share outputs)
         self.nstreams = max(1, streams)
         for k, c in enumerate(self.copies):
@@ -237,8 +263,17 @@ class GpuRunner:
         self.stream = torch.cuda.current_stream()
         self.streams = [self.stream] + [torch.cuda.Stream() for _ in range(self.nstreams - 1)]
 
+    def restore_ahead(self):
+        """rewriting configs: the copy launched two steps from now gets pristine bytes
+        (then >= 2 launches of other bytes lie between its restore and its parse)"""
+        if self.rewrites:
+            c = self.copies[(self.nstep + 2) % len(self.copies)]
+            c.bytes.copy_(self.pristine)
+
     def step(self, k):
-        self.copies[k % len(self.copies)].launch(self.stream)
+        self.restore_ahead()
+        self.copies[self.nstep % len(self.copies)].launch(self.stream)
+        self.nstep += 1
 
     def sync(self):
         self.torch.cuda.synchronize()
@@ -246,6 +281,8 @@ class GpuRunner:
     def timed(self, steps):
         """(wall seconds, mean launch ms from HIP events on the launch stream)"""
         torch = self.torch
+        if self.rewrites:
+            return self.timed_rewriting(steps)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         # the first record of timing events costs milliseconds on the host: do it outside the timed region
         ev0.record(self.stream)
@@ -265,6 +302,24 @@ class GpuRunner:
             print(f"bench diag: record {1e3 * (t1 - t0):.3f} ms, {steps} launches {1e3 * (t2 - t1):.3f} ms, "
                   f"record+sync {1e3 * (t3 - t2):.3f} ms", file=sys.stderr)
         return t3 - t0, ev0.elapsed_time(ev1) / steps
+
+    def timed_rewriting(self, steps):
+        """A config whose launches rewrite their bytes: each launch is bracketed by
+        its own events, the restore of a later copy (a D2D copy of the pristine
+        bytes) stays outside them.  (sum of launch seconds, mean launch ms)"""
+        torch = self.torch
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        torch.cuda.synchronize()
+        gc.collect()
+        for e0, e1 in evs:
+            self.restore_ahead()
+            e0.record(self.stream)
+            self.copies[self.nstep % len(self.copies)].launch(self.stream)
+            e1.record(self.stream)
+            self.nstep += 1
+        torch.cuda.synchronize()
+        ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+        return sum(ms) * 1e-3, sum(ms) / len(ms)
 
     def timed_pipelined(self, steps):
         """Wall seconds for `steps` launches, launch k on stream k % S: batch k+1
@@ -288,7 +343,10 @@ class GpuRunner:
         return time.perf_counter() - t0
 
     def ok_fraction(self):
-        res = self.copies[0].result()
+        last = self.copies[(self.nstep - 1) % len(self.copies)]   # its bytes were pristine when launched
+        res = last.result()
+        if res.http is not None:
+            return float((res.http["result"] == 1).mean()) if len(res.http) else 1.0
         return float((res.reqs["ret"] > 0).mean()) if len(res.reqs) else 1.0
 
 
@@ -365,8 +423,9 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="get256", choices=sorted(CONFIGS))
     ap.add_argument("--extra", default="auto", choices=["auto", "none"],
-                    help="auto: at N=1 also time configs 3 and 5 (extra_configs)")
+                    help="auto: at N=1 also time configs 3 and 5 and the chunked config (extra_configs)")
     ap.add_argument("--extra-steps", type=int, default=20)
+    ap.add_argument("--extras", default=",".join(EXTRA_KEYS), help="comma list of the extra configs to time")
     ap.add_argument("--copies", type=int, default=4)
     ap.add_argument("--per-gpu", type=int, default=0, help="requests per GPU (default: the config's 1M)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -402,7 +461,7 @@ def main(argv=None):
     r = run_config(args.config, args, rank, world, per_gpu, args.steps, args.warmup, dist)
     extra = {}
     if world == 1 and args.extra == "auto" and args.config == "get256":
-        for key in ("zipf", "post"):
+        for key in [k for k in args.extras.split(",") if k in EXTRA_KEYS]:
             e = run_config(key, args, rank, world, args.per_gpu or CONFIGS[key]["per_gpu"], args.extra_steps,
                            3, None)
             extra[key] = {"workload": CONFIGS[key]["name"], "value": round(e["total_alg"] / (e["kern_ms"] * 1e-3)
@@ -437,7 +496,7 @@ def main(argv=None):
             from e2e_pcie import e2e
             line["e2e"] = e2e(args.config, per_gpu, reps=3)
         if world == 1 and not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline([args.config] + [k for k in ("zipf", "post") if k in extra])
+            line["cpu_baseline"] = cpu_baseline([args.config] + [k for k in EXTRA_KEYS if k in extra])
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

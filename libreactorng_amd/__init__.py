@@ -32,7 +32,7 @@ IMPL_DFA, IMPL_EXACT, IMPL_DFA_LATE = 0, 1, 2
 RHP_NAME_NULL = 0xFFFF
 F_EXACT = 0x1
 
-GEN_TFB128, GEN_GET256, GEN_ZIPF, GEN_POST1K, GEN_FUZZ, GEN_FUZZ_HTTP = 1, 2, 3, 5, 100, 101
+GEN_TFB128, GEN_GET256, GEN_ZIPF, GEN_POST1K, GEN_CHUNKED, GEN_FUZZ, GEN_FUZZ_HTTP = 1, 2, 3, 5, 6, 100, 101
 
 # numpy views of the C records (rhp.h)
 REQ_DTYPE = np.dtype([("ret", "<i4"), ("method_len", "<u2"), ("path_off", "<u2"), ("path_len", "<u2"),

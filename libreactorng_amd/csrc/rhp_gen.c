@@ -9,6 +9,10 @@
  *               the 18 B minimal request), 0..32 headers, fill in path/values
  *   5  POST1K : 1 KiB POST with Content-Length body, 5 % seeded malformed
  *               (HTTP/2.0, CTL in value, SP before ':', CL+TE, missing ':')
+ *   6  CHUNKED: ~1 KiB POST, Transfer-Encoding: chunked, 1-8 chunks of seeded
+ *               data; chunk lines with extensions, OWS and either hex case;
+ *               5 % seeded malformed framing (bad hex, bare LF, a size past
+ *               the input, a coding other than chunked)
  *   100/101   : structured random edge cases for parity (every §8a hazard)
  * Every request depends only on (config, seed, index): shards are independent.
  */
@@ -199,6 +203,54 @@ static size_t gen_post(bld_t *b, rng_t *r, size_t *hdr_bytes)
   puts_(b, "\r\n\r\n");
   *hdr_bytes = b->len - start;
   for (size_t i = 0; i < body; i++) putc_(b, 'x');
+  return b->len - start;
+}
+
+/* ---------------- chunked POST (Transfer-Encoding: chunked) ---------------- */
+
+static void put_hex(bld_t *b, rng_t *r, uint32_t v)
+{
+  char t[16];
+  int n = 0;
+  const int upper_case = chance(r, 30);
+  do {
+    uint32_t d = v & 15u;
+    t[n++] = (char) (d < 10 ? '0' + d : (upper_case ? 'A' : 'a') + d - 10);
+    v >>= 4;
+  } while (v);
+  while (n) putc_(b, (uint8_t) t[--n]);
+}
+
+static size_t gen_chunked(bld_t *b, rng_t *r)
+{
+  size_t start = b->len;
+  int bad = chance(r, 5) ? 1 + (int) rndu(r, 5) : 0;
+  puts_(b, "POST /upload HTTP/1.1\r\n");
+  puts_(b, "Host: tfb-server:8080\r\n");
+  puts_(b, "Content-Type: application/octet-stream\r\n");
+  puts_(b, "Connection: keep-alive\r\n");
+  puts_(b, bad == 1 ? "Transfer-Encoding: gzip\r\n\r\n" : "Transfer-Encoding: chunked\r\n\r\n");
+  const uint32_t k = 1 + rndu(r, 8);                 /* data chunks */
+  const uint32_t payload = 640 + rndu(r, 256);       /* data bytes in all */
+  const uint32_t bad_at = rndu(r, k);                /* the chunk a framing error goes in */
+  uint32_t left = payload;
+  uint64_t word = 0;
+  for (uint32_t c = 0; c < k; c++) {
+    uint32_t sz = c + 1 == k ? left : 1 + rndu(r, left - (k - 1 - c));
+    left -= sz;
+    if (chance(r, 4)) putc_(b, ' ');                  /* OWS before the size (isblank) */
+    if (bad == 2 && c == bad_at) puts_(b, "zz");
+    else put_hex(b, r, bad == 4 && c == bad_at ? sz + 4096 : sz);
+    if (chance(r, 4)) putc_(b, '\t');                 /* OWS after it */
+    if (chance(r, 10)) puts_(b, ";ext=1");            /* chunk extension */
+    puts_(b, bad == 3 && c == bad_at ? "\n" : "\r\n");
+    for (uint32_t i = 0; i < sz; i++) {
+      if ((i & 7) == 0) word = rnd(r);
+      putc_(b, (uint8_t) (0x21 + (word >> (8 * (i & 7))) % 94));
+    }
+    puts_(b, "\r\n");
+  }
+  puts_(b, bad == 5 ? "0;last\n\r\n" : "0\r\n\r\n");
   return b->len - start;
 }
 
@@ -424,6 +476,7 @@ static size_t gen_one(int config, uint64_t seed, uint64_t idx, bld_t *b, size_t 
   case RHP_GEN_GET256: n = gen_tfb(b, &r, 138); break;
   case RHP_GEN_ZIPF: n = gen_zipf(b, &r); break;
   case RHP_GEN_POST1K: n = gen_post(b, &r, &h); break;
+  case RHP_GEN_CHUNKED: n = gen_chunked(b, &r); break;
   case RHP_GEN_FUZZ: n = gen_fuzz(b, &r, 0); break;
   case RHP_GEN_FUZZ_HTTP: n = gen_fuzz(b, &r, 1); break;
   default: return (size_t) -1;

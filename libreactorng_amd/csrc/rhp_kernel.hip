@@ -166,6 +166,89 @@ struct LineBytes {
   }
 };
 
+/* n body bytes from src to dst (dst <= src, offsets from `in`), forward: the
+ * in-place move of http_dechunk (http.c:155) for one thread.  Destination
+ * blocks are whole aligned 16-byte stores built from aligned 16-byte source
+ * lines (funnel-shifted by the constant src - dst), four blocks per memory
+ * round trip; the partial first and last blocks are byte stores, so no byte
+ * outside [dst, dst + n) -- another request's -- is written.  Loads read only
+ * source bytes no earlier store has reached (each block's source lies past its
+ * destination), apart from unused bytes of shared lines. */
+struct DevMove {
+  uint8_t *in;
+  __device__ void operator()(uint64_t dst, uint64_t src, uint64_t n) const
+  {
+    typedef __attribute__((address_space(1))) const u32x4 gq;
+    typedef __attribute__((address_space(1))) u32x4 gw;
+    if (n == 0 || dst == src) return;
+    const uintptr_t da = (uintptr_t) (in + dst), de = da + n, delta = (uintptr_t) (src - dst);
+    const uint32_t q = (uint32_t) (delta >> 2) & 3u, r = (uint32_t) delta & 3u;
+    /* block at destination A: source bytes [A + delta, A + delta + 16) from the
+     * lines at (A + delta) & ~15 and the one after it */
+    auto ld = [](uintptr_t a) -> u32x4 { return *reinterpret_cast<gq *>(a); };
+    auto block = [&](const u32x4 &l0, const u32x4 &l1) {
+      const uint32_t w[8] = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t lo = q == 0 ? w[j] : q == 1 ? w[j + 1] : q == 2 ? w[j + 2] : w[j + 3];
+        const uint32_t hi = q == 0 ? w[j + 1] : q == 1 ? w[j + 2] : q == 2 ? w[j + 3] : w[j + 4];
+        o[j] = __builtin_amdgcn_alignbyte(hi, lo, r);
+      }
+      return o;
+    };
+    auto partial = [&](uintptr_t A) {   /* bytes of block A inside [da, de): whole dwords, then bytes */
+      typedef __attribute__((address_space(1))) uint32_t gw1;
+      typedef __attribute__((address_space(1))) uint8_t gb1;
+      const uintptr_t s0 = (A + delta) & ~(uintptr_t) 15;
+      const u32x4 o = block(ld(s0), ld(s0 + 16));
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) {
+        const uintptr_t w = A + 4 * j;
+        if (w >= da && w + 4 <= de) {
+          *reinterpret_cast<gw1 *>(w) = o[j];
+        } else if (w + 4 > da && w < de) {
+#pragma unroll
+          for (uint32_t k = 0; k < 4; k++)
+            if (w + k >= da && w + k < de) *reinterpret_cast<gb1 *>(w + k) = (uint8_t) (o[j] >> (8 * k));
+        }
+      }
+    };
+    uintptr_t A = da & ~(uintptr_t) 15;
+    if (A != da || A + 16 > de) {   /* a partial first block */
+      partial(A);
+      A += 16;
+    }
+    constexpr int U = 4;
+    while (A + 16 * U <= de) {
+      const uintptr_t s0 = (A + delta) & ~(uintptr_t) 15;
+      u32x4 l[U + 1];
+#pragma unroll
+      for (int u = 0; u <= U; u++) l[u] = ld(s0 + 16 * u);
+#pragma unroll
+      for (int u = 0; u < U; u++) *reinterpret_cast<gw *>(A + 16 * u) = block(l[u], l[u + 1]);
+      A += 16 * U;
+    }
+    while (A + 16 <= de) {
+      const uintptr_t s0 = (A + delta) & ~(uintptr_t) 15;
+      *reinterpret_cast<gw *>(A) = block(ld(s0), ld(s0 + 16));
+      A += 16;
+    }
+    if (A < de) partial(A);
+  }
+};
+
+/* http_dechunk on the GPU (rhp_scalar.h dechunk_t): size lines read through the
+ * 16-byte line cache, payloads moved 16 bytes per store */
+struct DevDechunk {
+  __device__ int64_t operator()(uint8_t *in, uint64_t size, uint64_t *body_len, bool compact) const
+  {
+    LineBytes B{in, ~0ull, {0, 0, 0, 0}};
+    DevMove M{in};
+    return dechunk_t(B, M, size, body_len, compact);
+  }
+};
+
 /* Exact scalar path for one request (phr or http mode).  Only called from the
  * post-loop replay, where inlining it lets it reuse the loop's dead registers. */
 __device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64_t off, uint64_t len)
@@ -176,7 +259,7 @@ __device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64
   if (p.mode == RHP_MODE_HTTP) {
     rhp_http_t x;
     LineBytes B{p.bytes_rw + off, ~0ull, {0, 0, 0, 0}};
-    scalar_http_t(B, p.bytes_rw + off, len, p.max_headers, &r, h, p.hs_hdr, &x, p.compact);
+    scalar_http_t(B, p.bytes_rw + off, len, p.max_headers, &r, h, p.hs_hdr, &x, p.compact, DevDechunk{});
     p.http[i] = x;
   } else {
     LineBytes B{p.bytes + off, ~0ull, {0, 0, 0, 0}};
@@ -220,7 +303,9 @@ __device__ __forceinline__ void load28(const uint8_t *b, uint32_t (&d)[7])
 /* Case-insensitive compare of the first n <= 28 bytes of d (a header name
  * already in registers) with a lower-case literal: OR 0x20 folds letters; the
  * one non-letter, '-', could only collide with CR, which a parsed name cannot
- * hold (tchar only) */
+ * hold (tchar only).  For a literal of letters only ("chunked") the compare is
+ * exact for any bytes: x | 0x20 equals a lower-case letter only for that
+ * letter and its upper case. */
 template <uint32_t N>
 __device__ __forceinline__ bool name_is(const uint32_t (&d)[7], const char (&lit)[N])
 {
@@ -247,26 +332,34 @@ __device__ __forceinline__ uint64_t strtoull10_gpu(const uint8_t *s, const uint3
 
 /* http_frame (rhp_scalar.h) for the replay's common case, from the decode's
  * hints (cand, crec: see the decode state) -- GET, no candidate header, or one
- * that is Content-Length or neither; anything else takes http_frame.  Reads no
- * header record and no method byte: on batches larger than the caches those
- * re-reads are HBM traffic.  The candidate's name and value are loaded
- * together, one memory round trip. */
-__device__ __forceinline__ bool http_frame_fast(const uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x,
-                                                uint32_t cand, uint32_t crec_lo, uint32_t crec_hi)
+ * that is Content-Length or neither: the final record is written, kFrameDone.
+ * One candidate that is a Transfer-Encoding whose value is "chunked" (any
+ * case): kFrameChunked, the body (ret, len) is de-framed by the replay's second
+ * pass.  Anything else: kFrameSlow, http_frame.  Reads no header record and no
+ * method byte: on batches larger than the caches those re-reads are HBM
+ * traffic.  The candidate's name and value are loaded together, one memory
+ * round trip. */
+enum : int { kFrameDone = 0, kFrameSlow = 1, kFrameChunked = 2 };
+__device__ __forceinline__ int http_frame_fast(const uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x,
+                                               uint32_t cand, uint32_t crec_lo, uint32_t crec_hi)
 {
   const int64_t n = ret;
   rhp_http_t o = {1, 0, (uint64_t) n, 0};
   const uint32_t hdr = cand & 0x3fffffffu;
   if (!(cand & 0x40000000u) && hdr != 0) {   /* not GET (http.c:198-202), some candidate */
-    if ((cand >> 31) || (hdr & (hdr - 1)) != 0) return false;
+    if ((cand >> 31) || (hdr & (hdr - 1)) != 0) return kFrameSlow;
     /* a candidate's name is never RHP_NAME_NULL (its length is 14 or 17) */
     const uint32_t name_off = crec_lo & 0xffffu, name_len = crec_lo >> 16;
     const uint32_t value_off = crec_hi & 0xffffu, value_len = crec_hi >> 16;
     uint32_t dn[7], dv[7];
     load28(b + name_off, dn);
     load28(b + value_off, dv);
-    if (name_len == 17u && name_is(dn, "transfer-encoding")) return false;   /* chunked framing: the general path */
-    if (name_len == 14u && name_is(dn, "content-length") && value_len != 0) {
+    if (name_len == 17u && name_is(dn, "transfer-encoding") && value_len != 0) {
+      /* the only Transfer-Encoding and no Content-Length: "chunked" (http.c:221-224,
+       * data_equal_case) de-frames the body, anything else is -1 */
+      if (value_len == 7u && name_is(dv, "chunked")) return kFrameChunked;
+      o.result = -1; o.consumed = 0;
+    } else if (name_len == 14u && name_is(dn, "content-length") && value_len != 0) {
       const uint64_t size = strtoull10_gpu(b + value_off, dv, value_len);
       if (len < (uint64_t) n + size) {
         o.result = 0; o.consumed = 0;
@@ -276,7 +369,22 @@ __device__ __forceinline__ bool http_frame_fast(const uint8_t *b, uint64_t len, 
     }
   }
   *x = o;
-  return true;
+  return kFrameDone;
+}
+
+/* the chunked body of a request whose framing http_frame_fast settled
+ * (kFrameChunked): http_dechunk over (ret, len), http.c:225-230 */
+__device__ __forceinline__ void frame_chunked(uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x, bool compact)
+{
+  rhp_http_t o = {1, compact ? 1u : (uint32_t) RHP_BODY_CHUNKED_PENDING, 0, 0};
+  uint64_t blen = 0;
+  const int64_t size = DevDechunk{}(b + ret, len - (uint64_t) ret, &blen, compact);
+  if (size <= 0) {
+    o.result = (int32_t) size; o.body_kind = 0;
+  } else {
+    o.body_len = blen; o.consumed = (uint64_t) ret + (uint64_t) size;
+  }
+  *x = o;
 }
 
 /* Params pointers are generic in the kernel's view (they sit in a struct);
@@ -1283,7 +1391,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       } else {
         const uint32_t cand = h.hint[0];
         http_frame(p.bytes_rw + h.off, h.end - h.off, p.reqs[i], p.hdrs + (uint64_t) i * p.hs_req, p.hs_hdr,
-                   &p.http[i], (cand >> 31) ? ~0ull : (uint64_t) (cand & 0x3fffffffu), p.compact);
+                   &p.http[i], (cand >> 31) ? ~0ull : (uint64_t) (cand & 0x3fffffffu), p.compact, DevDechunk{});
       }
     };
     uint32_t *slow = reinterpret_cast<uint32_t *>(lds + kLdsTable);   /* the staging area, idle now */
@@ -1307,17 +1415,20 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       nx = head_at(k + WAVES * 64);
       const uint32_t f = what(cur);
       if (!f) continue;
-      bool later = (f & kHintExact) != 0;
-      if (!later)
-        later = !http_frame_fast(p.bytes_rw + cur.off, cur.end - cur.off, (int32_t) (cur.hint[1] & 0xffffu),
-                                 &p.http[i], cur.hint[0], cur.hint[2], cur.hint[3]);
+      const int fr = (f & kHintExact) ? kFrameSlow
+                                      : http_frame_fast(p.bytes_rw + cur.off, cur.end - cur.off,
+                                                        (int32_t) (cur.hint[1] & 0xffffu), &p.http[i], cur.hint[0],
+                                                        cur.hint[2], cur.hint[3]);
 #ifdef RHP_STAMPS
-      rp[3] += __popcll(__builtin_amdgcn_ballot_w64(!later));
+      rp[3] += __popcll(__builtin_amdgcn_ballot_w64(fr == kFrameDone));
 #endif
-      if (later) {
+      if (fr != kFrameDone) {
+        /* listed: the range-relative index, bit 31 = a chunked body to de-frame */
         const uint32_t at = atomicAdd(slow_n, 1u);
-        if (at < kSlowCap) slow[at] = i;
-        else finish_slow(i, cur);   /* list full (a range of > kSlowCap such requests) */
+        if (at < kSlowCap) slow[at] = (i - wg_lo) | (fr == kFrameChunked ? 0x80000000u : 0u);
+        else if (fr == kFrameChunked)   /* list full (a range of > kSlowCap such requests) */
+          frame_chunked(p.bytes_rw + cur.off, cur.end - cur.off, (int32_t) (cur.hint[1] & 0xffffu), &p.http[i], p.compact);
+        else finish_slow(i, cur);
       }
     }
 #ifdef RHP_STAMPS
@@ -1330,8 +1441,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #endif
     const uint32_t ns = min(*slow_n, kSlowCap);
     for (uint32_t k = tid; k < ns; k += WAVES * 64) {
-      const uint32_t i = slow[k];
-      finish_slow(i, head(i));
+      const uint32_t e = slow[k], i = wg_lo + (e & 0x7fffffffu);
+      const Head h = head(i);
+      if (e >> 31) frame_chunked(p.bytes_rw + h.off, h.end - h.off, (int32_t) (h.hint[1] & 0xffffu), &p.http[i], p.compact);
+      else finish_slow(i, h);
 #ifdef RHP_STAMPS
       rp[2] += __popcll(__builtin_amdgcn_ballot_w64(true));
 #endif
@@ -1358,7 +1471,7 @@ __global__ __launch_bounds__(256) void rhp_fixup_kernel(Params p, const rhp_sess
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_sessions; k += gridDim.x * blockDim.x) {
     const rhp_session_t ss = sessions[k];
     fixup_session_t(io, ss.piece_lo, ss.piece_hi, req_start, &results[k],
-                    [&](uint64_t at) { return LineBytes{p.bytes_rw + at, ~0ull, {0, 0, 0, 0}}; });
+                    [&](uint64_t at) { return LineBytes{p.bytes_rw + at, ~0ull, {0, 0, 0, 0}}; }, DevDechunk{});
   }
 }
 

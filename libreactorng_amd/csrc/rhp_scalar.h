@@ -295,51 +295,61 @@ RHP_HD int hexval(uint32_t c)
   return -1;
 }
 
-/* http_chunk_size + http_chunk (http.c:73-132): >0 bytes of this chunk
- * (size line + data + 2), 0 need more, -1 malformed; *data_off / *data_len */
-RHP_HD int64_t one_chunk(const uint8_t *in, uint64_t size, uint64_t *data_off, uint64_t *data_len)
+/* http_chunk_size + http_chunk (http.c:73-132) for the chunk whose size line
+ * starts at byte `at` of a body of `size` bytes, read through B (B(p) = body
+ * byte p): >0 bytes of this chunk (size line + data + 2), 0 need more, -1
+ * malformed; *data_off (from `at`) / *data_len.  Only the size line is read:
+ * the data bytes are skipped, and the reads stop at the line's LF. */
+template <class Bytes>
+RHP_HD int64_t one_chunk_t(Bytes &B, uint64_t at, uint64_t size, uint64_t *data_off, uint64_t *data_len)
 {
+  const uint64_t avail = size - at;
   uint64_t nl = 0;
-  while (nl < size && in[nl] != '\n') nl++;
-  if (nl == size) return 0;                      /* no '\n' yet */
-  const uint8_t *p = in;
-  while (is_ows(*p)) p++;
-  const uint8_t *digits = p;
-  while (hexval(*p) >= 0) p++;
+  while (nl < avail && B(at + nl) != '\n') nl++;   /* memchr(input, '\n') */
+  if (nl == avail) return 0;                      /* no '\n' yet */
+  uint64_t p = at;
+  while (is_ows(B(p))) p++;
+  const uint64_t digits = p;
+  while (hexval(B(p)) >= 0) p++;
   if (p == digits) return -1;
-  while (is_ows(*p)) p++;
-  if (*p == ';') {
-    while (*p != '\n') p++;
-    if (p[-1] != '\r') return -1;
+  const uint64_t digits_end = p;
+  while (is_ows(B(p))) p++;
+  if (B(p) == ';') {
+    p = at + nl;                                   /* while (*p != '\n') p++ */
+    if (B(p - 1) != '\r') return -1;
   } else {
-    if (*p != '\r') return -1;
+    if (B(p) != '\r') return -1;
     p++;
   }
-  if (*p != '\n') return -1;
+  if (B(p) != '\n') return -1;
   p++;
   uint64_t cs = 0;
   bool ovf = false;
-  for (const uint8_t *q = digits; hexval(*q) >= 0; q++) {
+  for (uint64_t q = digits; q < digits_end; q++) {
     ovf |= (cs >> 60) != 0;
-    cs = (cs << 4) | (uint64_t) hexval(*q);
+    cs = (cs << 4) | (uint64_t) hexval(B(q));
   }
   if (ovf || cs == ~0ull) return -1;             /* strtoul == ULONG_MAX */
-  uint64_t n = (uint64_t) (p - in);
-  if (n + 2 > size) return 0;
-  if (cs > size - n - 2) return 0;
+  const uint64_t n = p - at;
+  if (n + 2 > avail) return 0;
+  if (cs > avail - n - 2) return 0;
   *data_off = n;
   *data_len = cs;
   return (int64_t) (cs + n + 2);
 }
 
-/* http_dechunk (http.c:134-160): validate, then compact payloads in place.
- * compact = false (speculative batches, rhp.h RHP_BATCH_SPECULATIVE): validate
- * only and report the payload length; nothing is written */
-RHP_HD int64_t dechunk(uint8_t *in, uint64_t size, uint64_t *body_len, bool compact = true)
+/* http_dechunk (http.c:134-160): validate every chunk, then move the payloads
+ * down in place, chunk by chunk (dst <= src: the compacted body never passes
+ * the next size line).  B reads the body (B(p) = body byte p), move(dst, src, n)
+ * copies n body bytes forward.  compact = false (speculative batches, rhp.h
+ * RHP_BATCH_SPECULATIVE): validate only and report the payload length; nothing
+ * is written. */
+template <class Bytes, class Move>
+RHP_HD int64_t dechunk_t(Bytes &B, Move &move, uint64_t size, uint64_t *body_len, bool compact)
 {
   uint64_t off = 0, doff = 0, dlen = 0, sum = 0;
   do {
-    int64_t n = one_chunk(in + off, size - off, &doff, &dlen);
+    int64_t n = one_chunk_t(B, off, size, &doff, &dlen);
     if (n <= 0) return n;
     off += (uint64_t) n;
     sum += dlen;
@@ -351,9 +361,8 @@ RHP_HD int64_t dechunk(uint8_t *in, uint64_t size, uint64_t *body_len, bool comp
   uint64_t total = 0;
   off = 0;
   do {
-    int64_t n = one_chunk(in + off, size - off, &doff, &dlen);
-    const uint8_t *src = in + off + doff;
-    for (uint64_t i = 0; i < dlen; i++) in[total + i] = src[i];  /* dst <= src: forward copy */
+    int64_t n = one_chunk_t(B, off, size, &doff, &dlen);
+    move(total, off + doff, dlen);
     off += (uint64_t) n;
     total += dlen;
   } while (dlen);
@@ -361,14 +370,38 @@ RHP_HD int64_t dechunk(uint8_t *in, uint64_t size, uint64_t *body_len, bool comp
   return (int64_t) off;
 }
 
+/* the byte-wise form (host) */
+struct PlainMove {
+  uint8_t *in;
+  RHP_HDM void operator()(uint64_t dst, uint64_t src, uint64_t n) const
+  {
+    for (uint64_t i = 0; i < n; i++) in[dst + i] = in[src + i];   /* dst <= src: forward copy */
+  }
+};
+RHP_HD int64_t dechunk(uint8_t *in, uint64_t size, uint64_t *body_len, bool compact = true)
+{
+  PlainBytes B{in};
+  PlainMove M{in};
+  return dechunk_t(B, M, size, body_len, compact);
+}
+
+/* http_dechunk over the body at `in` (size bytes).  Plain: the byte-wise form;
+ * the GPU passes its own (line-cached size-line reads, 16-byte moves). */
+struct PlainDechunk {
+  RHP_HDM int64_t operator()(uint8_t *in, uint64_t size, uint64_t *body_len, bool compact) const
+  {
+    return dechunk(in, size, body_len, compact);
+  }
+};
+
 /* Framing decision given a successful phr parse (n = ret > 0) of a request of
  * len bytes at b: get = the method is "GET"; hv / nh = its headers.
  * cand: the header indices whose name could be Transfer-Encoding or
  * Content-Length (name length 17 or 14), as found by the kernel's decode; ~0
  * checks every header */
-template <class HV>
+template <class HV, class DC = PlainDechunk>
 RHP_HD void http_frame_t(uint8_t *b, uint64_t len, int64_t n, bool get, const HV &hv, uint32_t nh, rhp_http_t *x,
-                         uint64_t cand = ~0ull, bool compact = true)
+                         uint64_t cand = ~0ull, bool compact = true, const DC &dc = DC())
 {
   /* one framing candidate (the common case): its name is read together with
    * its value digits, so the GPU replay makes fewer memory round trips */
@@ -409,18 +442,19 @@ RHP_HD void http_frame_t(uint8_t *b, uint64_t len, int64_t n, bool get, const HV
     for (uint32_t i = 0; eq && i < 7; i++) eq = upper(v[i]) == (uint32_t) ch[i];
     if (!eq) { x->result = -1; x->consumed = 0; return; }
     uint64_t blen = 0;
-    int64_t size = dechunk(b + n, len - (uint64_t) n, &blen, compact);
+    int64_t size = dc(b + n, len - (uint64_t) n, &blen, compact);
     if (size <= 0) { x->result = (int32_t) size; x->consumed = 0; return; }
     x->body_kind = compact ? 1u : RHP_BODY_CHUNKED_PENDING;
     x->body_len = blen; x->consumed = (uint64_t) n + (uint64_t) size;
   }
 }
 
+template <class DC = PlainDechunk>
 RHP_HD void http_frame(uint8_t *b, uint64_t len, const rhp_req_t &r, const rhp_hdr_t *h, uint64_t hs, rhp_http_t *x,
-                       uint64_t cand = ~0ull, bool compact = true)
+                       uint64_t cand = ~0ull, bool compact = true, const DC &dc = DC())
 {
   const bool get = r.method_len == 3 && ((b[r.method_off] == 'G') & (b[r.method_off + 1] == 'E') & (b[r.method_off + 2] == 'T'));
-  http_frame_t(b, len, r.ret, get, HdrsRec{b, h, hs}, r.num_headers, x, cand, compact);
+  http_frame_t(b, len, r.ret, get, HdrsRec{b, h, hs}, r.num_headers, x, cand, compact, dc);
 }
 
 /* phr status -> http_read_request result when the parse gave no request
@@ -429,15 +463,15 @@ RHP_HD void http_frame(uint8_t *b, uint64_t len, const rhp_req_t &r, const rhp_h
 RHP_HD int32_t http_result_of(int n) { return n == kBad ? -1 : n == RHP_RET_TOOLONG ? RHP_RET_TOOLONG : 0; }
 
 /* Whole http_read_request for one request. */
-template <class Bytes>
+template <class Bytes, class DC = PlainDechunk>
 RHP_HD void scalar_http_t(Bytes &B, uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, uint64_t hs,
-                          rhp_http_t *x, bool compact = true)
+                          rhp_http_t *x, bool compact = true, const DC &dc = DC())
 {
   int n = scalar_phr_t(B, len, max, r, h, hs);
   x->body_kind = 0; x->consumed = 0; x->body_len = 0;
   if (len == 0) { x->result = 0; return; }
   if (n <= 0) { x->result = http_result_of(n); return; }
-  http_frame(b, len, *r, h, hs, x, ~0ull, compact);
+  http_frame(b, len, *r, h, hs, x, ~0ull, compact, dc);
 }
 RHP_HD void scalar_http(uint8_t *b, uint64_t len, uint32_t max, rhp_req_t *r, rhp_hdr_t *h, uint64_t hs, rhp_http_t *x)
 {
@@ -461,9 +495,9 @@ struct FixupIO {
   uint32_t max_headers;
 };
 
-template <class MakeBytes>
+template <class MakeBytes, class DC = PlainDechunk>
 RHP_HD void fixup_session_t(const FixupIO &io, uint32_t p_lo, uint32_t p_hi, uint64_t *req_start,
-                            rhp_session_result_t *out, MakeBytes mk)
+                            rhp_session_result_t *out, MakeBytes mk, const DC &dc = DC())
 {
   const uint64_t b_lo = io.off[p_lo], b_hi = io.off[p_hi];
   uint64_t pos = b_lo;
@@ -485,7 +519,7 @@ RHP_HD void fixup_session_t(const FixupIO &io, uint32_t p_lo, uint32_t p_hi, uin
         /* a true request boundary now: de-frame its chunked body in place
          * (http.c:225-229, the memmove of http_dechunk) */
         uint64_t blen = 0;
-        (void) dechunk(io.bytes_rw + pos + (uint64_t) r.ret, x.consumed - (uint64_t) r.ret, &blen, true);
+        (void) dc(io.bytes_rw + pos + (uint64_t) r.ret, x.consumed - (uint64_t) r.ret, &blen, true);
         x.body_kind = 1;
       }
       if (j != slot) {
@@ -498,7 +532,7 @@ RHP_HD void fixup_session_t(const FixupIO &io, uint32_t p_lo, uint32_t p_hi, uin
     } else {
       auto B = mk(pos);
       scalar_http_t(B, io.bytes_rw + pos, b_hi - pos, io.max_headers, &io.reqs[slot],
-                    io.hdrs + (uint64_t) slot * io.hs_req, io.hs_hdr, &x, true);
+                    io.hdrs + (uint64_t) slot * io.hs_req, io.hs_hdr, &x, true, dc);
       io.http[slot] = x;
     }
     req_start[slot] = pos;

@@ -16,7 +16,9 @@ Full-size BASELINE configs (1M requests; config 4 as 8 shards of 1M) are too
 large to store: full_digests.json keeps the sha256 of the reference's canonical
 record stream for each, which the GPU tests recompute from the kernel's output.
 
-usage: python tests/golden/make_golden.py [--no-full]
+usage: python tests/golden/make_golden.py [--no-full] [--only NAME ...]
+  --only: (re)make just the named sets of SETS / FULL, keeping every other
+          fixture and manifest entry as it is
 """
 import hashlib
 import json
@@ -44,6 +46,7 @@ SETS = [
     ("zipf_phr_h32", rhp.GEN_ZIPF, 1024, 0x5EED0003, 32, rhp.MODE_PHR),
     ("zipf_phr_h16", rhp.GEN_ZIPF, 1024, 0x5EED0003, 16, rhp.MODE_PHR),
     ("post1k_http", rhp.GEN_POST1K, 1024, 0x5EED0005, 16, rhp.MODE_HTTP),
+    ("chunked_http_h16", rhp.GEN_CHUNKED, 2048, 0x5EED0006, 16, rhp.MODE_HTTP),
     ("fuzz_phr_h16", rhp.GEN_FUZZ, 4000, 11, 16, rhp.MODE_PHR),
     ("fuzz_phr_h2", rhp.GEN_FUZZ, 1500, 13, 2, rhp.MODE_PHR),
     ("fuzz_phr_h0", rhp.GEN_FUZZ, 1500, 14, 0, rhp.MODE_PHR),
@@ -68,6 +71,7 @@ FULL = [
     ("config3_zipf_h32", rhp.GEN_ZIPF, 0, 1 << 20, 0x5EED0003, 32, rhp.MODE_PHR),
     ("config3_zipf_h16", rhp.GEN_ZIPF, 0, 1 << 20, 0x5EED0003, 16, rhp.MODE_PHR),
     ("config5_post1k_http_h16", rhp.GEN_POST1K, 0, 1 << 20, 0x5EED0005, 16, rhp.MODE_HTTP),
+    ("chunked_post_http_h16", rhp.GEN_CHUNKED, 0, 1 << 20, 0x5EED0006, 16, rhp.MODE_HTTP),
 ] + [(f"config4_get256_shard{g}of8", rhp.GEN_GET256, g << 20, 1 << 20, 0x5EED0002, 16, rhp.MODE_PHR)
      for g in range(8)]
 
@@ -132,22 +136,41 @@ def last_len_set():
             "input_sha256": hashlib.sha256(buf.tobytes()).hexdigest()}
 
 
-def full_digests():
-    out = {}
+def full_digests(only=None):
+    path = os.path.join(HERE, "full_digests.json")
+    out = json.load(open(path))["sets"] if only else {}
     for name, cfg, lo, n, seed, maxh, mode in FULL:
+        if only and name not in only:
+            continue
         buf, off = rhp.generate(cfg, n, seed, lo=lo)
-        reqs, hdrs, http, _ = run_reference(buf, off, maxh, mode)
+        reqs, hdrs, http, rw = run_reference(buf, off, maxh, mode)
         r, h, x = to_rhp(reqs, hdrs, http, mode)
         out[name] = {"config": cfg, "lo": lo, "n": n, "seed": seed, "max_headers": maxh, "mode": mode,
                      "input_sha256": hashlib.sha256(buf.tobytes()).hexdigest(),
                      "records_sha256": record_digest(r, h, x), "ret_ok": int((r["ret"] > 0).sum())}
+        if cfg == rhp.GEN_CHUNKED:   # http_dechunk rewrites the bodies in place: their bytes are output too
+            out[name]["bytes_out_sha256"] = hashlib.sha256(rw.tobytes()).hexdigest()
         print(name, out[name]["records_sha256"][:16], out[name]["ret_ok"])
     json.dump({"producer": "oracle/_ref/libref.so via oracle/ref_harness.c (the reference compiled from "
                "/root/reference)", "digest": "tests/golden_sets.py record_digest over to_rhp records",
-               "sets": out}, open(os.path.join(HERE, "full_digests.json"), "w"), indent=1)
+               "sets": out}, open(path, "w"), indent=1)
+
+
+def main_only(only):
+    mpath = os.path.join(HERE, "manifest.json")
+    m = json.load(open(mpath))
+    for name, cfg, n, seed, maxh, mode in SETS:
+        if name in only:
+            buf, off = rhp.generate(cfg, n, seed)
+            save_set(m["sets"], name, buf, off, maxh, mode, {"config": cfg, "n": n, "seed": seed})
+    json.dump(m, open(mpath, "w"), indent=1)
+    if any(name in only for name, *_ in FULL):
+        full_digests(only)
 
 
 def main():
+    if "--only" in sys.argv:
+        return main_only(set(sys.argv[sys.argv.index("--only") + 1:]))
     check_vectors()
     manifest = {}
     for name, builder, shift, maxh, mode in BUILT:

@@ -116,14 +116,19 @@ def test_pointer_parser_last_len_matches_reference_golden():
             assert hs == want, i
 
 
-@pytest.mark.parametrize("name", ["config2_get256_h16", "config5_post1k_http_h16", "config4_get256_shard7of8"])
+@pytest.mark.parametrize("name", ["config2_get256_h16", "config5_post1k_http_h16", "config4_get256_shard7of8",
+                                  "chunked_post_http_h16"])
 def test_oracle_full_size_matches_reference_digest(name):
     """The restatement at BASELINE full size (1M requests) against the digest of
-    the compiled reference's record stream (tests/golden/full_digests.json)."""
+    the compiled reference's record stream (tests/golden/full_digests.json), and
+    of the de-chunked bytes where http_dechunk rewrote them."""
     spec = FULL[name]
     buf, off = inputs(spec)
-    got = to_rhp(*run_oracle(buf, off, spec["max_headers"], spec["mode"])[:3], spec["mode"])
+    reqs, hdrs, http, out = run_oracle(buf, off, spec["max_headers"], spec["mode"])
+    got = to_rhp(reqs, hdrs, http, spec["mode"])
     assert record_digest(*got) == spec["records_sha256"]
+    if "bytes_out_sha256" in spec:
+        assert hashlib.sha256(out.tobytes()).hexdigest() == spec["bytes_out_sha256"]
 
 
 @pytest.mark.skipif(not os.path.isdir("/root/reference"), reason="needs the reference sources (dev container)")

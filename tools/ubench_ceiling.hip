@@ -163,6 +163,35 @@ __global__ void groupw(const uint8_t *buf, uint8_t *reqs, uint8_t *hdrs, uint32_
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
+/* group, with the records of group g stored after the loads of group g + 1
+ * are issued: vmcnt counts loads and stores together in issue order, so in
+ * `group` each group's first load wait also waits for the previous group's
+ * stores; here the stores are younger than the loads waited for */
+template <int U>
+__global__ void groupp(const uint8_t *buf, uint8_t *reqs, uint8_t *hdrs, uint32_t *out)
+{
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t waves = (uint64_t) gridDim.x * (blockDim.x >> 6);
+  uint32_t acc = 0, prev_acc = 0;
+  uint64_t prev_i = ~0ull;
+  for (uint64_t g = (uint64_t) blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); g < kReqs / 64; g += waves) {
+    const uint8_t *b = buf + g * 16384 + 16 * lane;
+    acc = 0;
+    for (int j = 0; j < 16; j += U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load((gq *) (uintptr_t) (b + 1024 * (j + u)));
+      if (j == 0 && prev_i != ~0ull) write_records(reqs, hdrs, prev_i, prev_acc);
+#pragma unroll
+      for (int u = 0; u < U; u++) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+    }
+    prev_i = g * 64 + lane;
+    prev_acc = acc;
+  }
+  if (prev_i != ~0ull) write_records(reqs, hdrs, prev_i, prev_acc);
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
 /* writes only: 48 MB with 16 B per lane, contiguous */
 __global__ void wonly(const uint8_t *, uint8_t *reqs, uint8_t *hdrs, uint32_t *out)
 {
@@ -241,6 +270,8 @@ int main()
       GROUPW(8, 2, 256, 1024);
       GROUPW(8, 3, 256, 1024);
       GROUPW(8, 4, 256, 1024);
+      run("groupp U8 (stores after the next loads)", [&](uint8_t *in, uint32_t *) { hipLaunchKernelGGL((groupp<8>), dim3(256), dim3(1024), 0, 0, in, b.reqs, b.hdrs, b.out); }, b, false);
+      run("groupp U4 (stores after the next loads)", [&](uint8_t *in, uint32_t *) { hipLaunchKernelGGL((groupp<4>), dim3(256), dim3(1024), 0, 0, in, b.reqs, b.hdrs, b.out); }, b, false);
       run("wonly 48 MB", [&](uint8_t *in, uint32_t *) { hipLaunchKernelGGL(wonly, dim3(256 * 4), dim3(256), 0, 0, in, b.reqs, b.hdrs, b.out); }, b, false);
     }
     return 0;

@@ -68,7 +68,6 @@ enum State : uint32_t {
   S_METHOD0, S_METHOD, S_PATH0, S_PATH,
   S_V1, S_V2, S_V3, S_V4, S_V5, S_V6, S_V7, S_V8_0, S_V8_1, S_CRLF_RL,
   S_LINE0, S_NAME, S_VAL0, S_VALUE, S_VWS, S_VCR, S_END_CR,
-  S_SEEK,        /* the second half of a split request (rhp_kernel.hip): skip to the first LF */
   S_NUM_PLAIN,
   /* event rows (an event fires on the transition that enters them) */
   S_DONE_E = S_NUM_PLAIN, S_ERR_E,             /* terminal events */
@@ -180,10 +179,6 @@ constexpr uint32_t step(uint32_t s, uint32_t c)
   case S_VCR: return c == '\n' ? S_LINE_E : S_ERR_E;
   case S_END_CR:    /* empty line ends the headers (:268-275) */
     return c == '\n' ? S_DONE_E : S_ERR_E;
-  case S_SEEK:      /* a split request's second half starts inside a line: every byte up to
-                       the line's LF was checked by the first half's lane; after the LF a
-                       header line starts (the EOL event marks where) */
-    return c == '\n' ? S_LINE_E : S_SEEK;
   default: return S_SLOW;
   }
 }

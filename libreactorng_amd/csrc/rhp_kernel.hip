@@ -95,29 +95,13 @@ enum : uint32_t {
   /* workgroup pool area after the staging buffers: counters, then the long-
    * request bitmap (ranges up to kOrderSpan requests) and list */
   kPoolWords = 8,                                /* counter, replay flag, long-list length, long-list
-                                                    cursor, slow-list length, defer-list length,
-                                                    split-list length, split-list cursor */
+                                                    cursor, slow-list length, defer-list length */
   kOrderSpan = 8192,
-  kListCap = 1024,
-  /* split requests (early form, uneven ranges): a request of kSplitMin..kSplitMax
-   * bytes is walked by two lanes, the head from its start and the tail from the
-   * middle window on ("Split requests"); the split list (pairs
-   * of u16 entries, bit 15 = tail) and the tails' results live in the staging
-   * buffer of the last wave, which uneven ranges leave idle */
-  kSplitMin = 2048,
-  kSplitMax = 32768,
-  kSplitCap = 1024,                              /* pairs */
-  kSplitHead = 0x4000u,                          /* reqs[i].flags: the head stopped at the junction */
-  kMergeBytes = 512,                             /* LDS scratch per merging thread: 64 records */
+  kListCap = 1536,
   kDeferCap = 480,                               /* the replay's list (defer) */
   kPoolBytes = 4 * kPoolWords + kOrderSpan / 8 + 2 * kListCap + 2 * kDeferCap
 };
 static_assert(idx2(S_DONE, 0) == kPark, "parked lanes sit in DONE");
-static_assert(2 * kSplitCap * 2 + kSplitCap * 4 <= kStageWave, "split list and tail results fit one wave's staging");
-static_assert(kSplitMax < RHP_MAX_LEN, "a tail's terminal fits 16 bits");
-
-/* the window a split request's tail starts at: the middle of its windows */
-__device__ __forceinline__ uint32_t split_m(uint32_t len, uint32_t mis) { return ((len + mis + kBlock - 1u) / kBlock) / 2u; }
 
 /* LDS byte address of part q (16 B) of lane w's window inside the staging
  * buffer.  The LDS-DMA loads of a wave write lane-linearly (1 KiB per
@@ -523,12 +507,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   uint16_t *long_list = reinterpret_cast<uint16_t *>(long_bits + kOrderSpan / 32);
   const bool order_on = wg_hi - wg_lo <= kOrderSpan;
   bool list_dry = !order_on;
-  constexpr bool kSplit = !LATE && !HTTP;   /* split requests: the phr early form only */
-  uint32_t *split_n = wg_counter + 6, *split_next = wg_counter + 7;
-  uint16_t *split_list = reinterpret_cast<uint16_t *>(lds + kLdsTable + (WAVES - 1) * kStageWave);
-  uint32_t *tinfo = reinterpret_cast<uint32_t *>(split_list + 2 * kSplitCap);   /* per pair: the tail's result */
-  const bool split_on = kSplit && order_on && p.last_len == nullptr && p.max_headers > 0;
-  bool split_dry = true;
   bool listed = false;   /* the range was scanned: skip the listed requests in order */
   bool first_iter = true;   /* the list is complete only after the scan (before the loop) */
   bool pool_dry = wg_lo >= wg_hi;
@@ -571,8 +549,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   bool pend_ok = false;                /* pend: the lane's next request */
   uint32_t pend = 0;
   uint32_t pend_o0 = 0, pend_o1 = 0;   /* low dwords of offsets[pend], offsets[pend+1] as loaded */
-  uint32_t pend_sp = 0, w_sp = 0;      /* split tag of pend / wcur: 0, or 0x10000 | split-list position
-                                          (bit 0: the tail) */
   uint32_t nw = 0;                     /* next window: byte offset from base | kind (0 none, 1
                                           continuation, 2 first window of pend); windows are 4-aligned */
   u32x4 W[kParts];                     /* the window in registers */
@@ -602,22 +578,12 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * number carried into the next window.  fr flags (kFr*), fv the number. */
   uint32_t fr = 0;
   uint64_t fv = 0;
-  /* split requests (kSplit): d_sp the decoded request's split tag; a head stops
-   * decoding after the first line end at or after djpos (hj: reached), a tail
-   * takes its first event (the LF its seek ends at) as the start of its first
-   * line (dseek: not yet) and stores its records from the last slot down */
-  uint32_t d_sp = 0;
-  int32_t djpos = 0;
-  bool hj = false, dseek = false;
-  bool split_wave = false;   /* wave-uniform: some lane decodes a split request (the split code runs) */
-  bool dterm = false;   /* the decoded window holds the request's terminal: a head decodes it all
-                           (its junction would lie before the end: it finishes the request itself) */
 #pragma unroll
   for (int w = 0; w < (int) kEvWords; w++) ev[w] = evp[w] = 0;
 
   /* give every lane without a pending request one from the pool; the offsets
    * loads are only consumed at the top of the next block */
-  auto take = [&](uint32_t i, uint32_t sp = 0) {
+  auto take = [&](uint32_t i) {
     /* only the low dwords: the range is below 4 GiB, so offsets relative to
      * `base` and lengths are exact modulo 2^32 */
     const uint32_t *o = reinterpret_cast<const uint32_t *>(p.offsets + i);
@@ -625,33 +591,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     pend_o0 = *GLOBAL(const uint32_t, o);
     pend_o1 = *GLOBAL(const uint32_t, o + 2);
     pend_ok = true;
-    pend_sp = sp;
-  };
-  /* the first window of a request taken from the pool (a tail's: its middle one) */
-  auto pend_window = [&](uint32_t o0, uint32_t o1, uint32_t sp) -> uint32_t {
-    uint32_t a = (o0 & ~3u) - (uint32_t) base;
-    if (kSplit && (sp & 1u)) a += kBlock * split_m(o1 - o0, o0 & 3u);
-    return a | 2u;
   };
   auto refill_pend = [&]() {
     uint64_t want = __ballot(!pend_ok);
-    if (!want || (pool_dry && list_dry && split_dry)) return;
-    if (kSplit && !split_dry && !first_iter) {   /* split pairs first: the longest requests */
-      const uint32_t cnt = (uint32_t) __popcll(want);
-      uint32_t b0 = 0;
-      if (lane == 0) b0 = atomicAdd(split_next, cnt);
-      b0 = __builtin_amdgcn_readfirstlane(b0);
-      const uint32_t ns = min(*split_n, 2u * (uint32_t) kSplitCap);
-      if (b0 + cnt >= ns) split_dry = true;
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
-      if (!pend_ok && b0 + rank < ns) {
-        const uint32_t e = split_list[b0 + rank];
-        take(wg_lo + (e & 0x1fffu), 0x10000u | (b0 + rank));
-      }
-      want = __ballot(!pend_ok);
-      if (!want) return;
-    }
-    if (!list_dry && !first_iter) {   /* the long list next */
+    if (!want || (pool_dry && list_dry)) return;
+    if (!list_dry && !first_iter) {   /* the long list first */
       const uint32_t cnt = (uint32_t) __popcll(want);
       uint32_t b0 = 0;
       if (lane == 0) b0 = atomicAdd(list_next, cnt);
@@ -684,17 +628,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     for (uint32_t k = tid; k < span_n; k += WAVES * 64) {
       const uint64_t o0 = p.offsets[wg_lo + k], o1 = p.offsets[wg_lo + k + 1];
       if ((o1 - o0) * span_n > twice) {
-        const uint64_t len = o1 - o0;
-        if (split_on && len >= kSplitMin && len <= kSplitMax) {
-          const uint32_t at = atomicAdd(split_n, 2u);
-          if (at < 2u * kSplitCap) {
-            split_list[at] = (uint16_t) k;
-            split_list[at + 1] = (uint16_t) (k | 0x8000u);
-            tinfo[at >> 1] = 0;
-            atomicOr(&long_bits[k >> 5], 1u << (k & 31));
-            continue;
-          }
-        }
         const uint32_t at = atomicAdd(list_n, 1u);
         if (at < kListCap) {
           long_list[at] = (uint16_t) k;
@@ -735,7 +668,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * window from dcur and nh, not carried across the walk; the host keeps
    * n * max_headers below 2^32) */
   uint32_t hx = 0;
-  uint32_t hstep = p.hs_hdr;   /* hx step per record (a split tail: -hs_hdr, from the last slot down) */
   auto word = [&](uint32_t m, uint32_t base) {
     m &= dstop - 1u;   /* nothing after a max_headers stop */
     if (!__builtin_amdgcn_ballot_w64(m != 0)) return;
@@ -748,14 +680,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       m &= m - v;
       const uint32_t k = v ? kn & 7u : 7u;
       const uint32_t mv = ((ep - pe - 9u) & 1u) << 3;
-      if (kSplit && split_wave) {
-        /* a split head whose junction (the first LF at or after djpos) is the
-         * request line's LF (PE + 10): the head's part ends with this line */
-        const bool jrl = k == 2u && d_sp != 0 && !(d_sp & 1u) && !hj && !dterm && pe + 10u >= (uint32_t) djpos;
-        m = jrl ? 0u : m;
-        dstop = jrl ? 1u : dstop;
-        hj = hj || jrl;
-      }
       rl = k == 1u ? me | ((ep - me - 1u) << 16) : rl;
       ls = k == 1u ? ep + 11u : ls;
       me = k == 0u ? ep : me;
@@ -770,22 +694,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const uint32_t odd = m & px;
     uint32_t com = t ? m ^ odd : odd;    /* t = 1: the word opens with an EOL */
     uint32_t eolm = m ^ com;
-    if (kSplit && split_wave) {
-      /* a split head ends after the first line end at or after djpos: the events
-       * past it are the tail's */
-      const bool head = d_sp != 0 && !(d_sp & 1u) && !hj && !dterm;
-      if (__builtin_amdgcn_ballot_w64(head && base + 31u >= (uint32_t) djpos)) {
-        const uint32_t sh = (uint32_t) djpos > base ? (uint32_t) djpos - base : 0u;
-        const uint32_t f = head && sh < 32u ? eolm & (~0u << sh) : 0u;
-        if (f) {
-          const uint32_t keep = ~0u >> (31u - (uint32_t) __builtin_ctz(f));
-          eolm &= keep;
-          com &= keep;
-          hj = true;
-          dstop = 1u;
-        }
-      }
-    }
     if (!__builtin_amdgcn_ballot_w64(nh + (uint32_t) __builtin_popcount(eolm) >= maxh)) {
       /* no lane can reach max_headers in this word: no capacity checks */
       /* Straight-line body for every lane (a masked `if` costs more in copies
@@ -809,7 +717,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         eolm &= eolm - 1u;
         ls = has ? e + 1u : ls;
         nh += (uint32_t) has;
-        hx += has ? hstep : 0u;
+        hx += has ? p.hs_hdr : 0u;
         t = has ? 0u : t;
       }
       /* a colon left open at the end of the word: a later word (or window) has its LF */
@@ -843,7 +751,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       eolm = stop ? 0u : rec ? eolm & (eolm - 1u) : eolm;
       ls = rec ? e + 1u : ls;
       nh += rec ? 1u : 0u;
-      hx += rec ? hstep : 0u;
+      hx += rec ? p.hs_hdr : 0u;
       t = rec ? 0u : t;
     }
     const bool open = com != 0;
@@ -982,17 +890,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     term_pos = 0xffffffffu;
     dstop = 0;
     hx = dcur * p.hs_req + nh * p.hs_hdr;
-    if constexpr (kSplit) {
-      split_wave = __builtin_amdgcn_ballot_w64(d_sp != 0) != 0;
-      hstep = p.hs_hdr;
-    }
-    if (kSplit && split_wave) {
-      dterm = term_ev;
-      const bool tail = (d_sp & 1u) != 0;
-      hx = tail ? dcur * p.hs_req + (maxh - 1u - nh) * p.hs_hdr : hx;
-      hstep = tail ? 0u - p.hs_hdr : p.hs_hdr;
-      dstop = hj ? 1u : 0u;
-    }
     if (term_ev) {   /* the terminal is the window's last event: take it off the mask */
       const int q = mq[3] ? 3 : mq[2] ? 2 : mq[1] ? 1 : 0;
       uint32_t w = q == 3 ? mq[3] : q == 2 ? mq[2] : q == 1 ? mq[1] : mq[0];
@@ -1001,19 +898,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       w &= ~(1u << bt);
 #pragma unroll
       for (int k = 0; k < (int) kEvWords; k++) mq[k] = k == q ? w : mq[k];
-    }
-    if (kSplit && split_wave) {
-      /* a tail's first event is the LF its seek ended at: its first line starts after it */
-      if (__builtin_amdgcn_ballot_w64(dseek && (mq[0] | mq[1] | mq[2] | mq[3]) != 0)) {
-        const int q = mq[0] ? 0 : mq[1] ? 1 : mq[2] ? 2 : 3;
-        const uint32_t w = q == 0 ? mq[0] : q == 1 ? mq[1] : q == 2 ? mq[2] : mq[3];
-        if (dseek && w) {
-          ls = (uint32_t) dpos + 32u * (uint32_t) q + (uint32_t) __builtin_ctz(w) + 1u;
-          dseek = false;
-#pragma unroll
-          for (int k = 0; k < (int) kEvWords; k++) mq[k] = k == q ? w & (w - 1u) : mq[k];
-        }
-      }
     }
   };
   /*
@@ -1027,40 +911,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const uint32_t e = st_prev;
     const bool ovfl = ovf != 0;
     const bool term_ev = is_done2(e) || is_err2(e);
-    const bool fin = dhas && (ovfl || is_slow2(e) || term_ev || (uint32_t) dpos + kBlock >= dlen || hj);
+    const bool fin = dhas && (ovfl || is_slow2(e) || term_ev || (uint32_t) dpos + kBlock >= dlen);
     if (!fin) return false;
-    if constexpr (kSplit) {
-      if (d_sp & 1u) {
-        /* a tail: its result for the merge after the loop (it never writes reqs) */
-        const bool tok = !ovfl && is_done2(e) && term_pos < dlen;
-        const bool tbad = ovfl ? ovf - 1u < dlen : is_err2(e) && term_pos < dlen;
-        const uint32_t status = tok ? 1u : tbad ? 2u : 3u;
-        tinfo[(d_sp & 0xffffu) >> 1] = (term_pos & 0xffffu) | (min(nh, 255u) << 16) | (status << 24);
-        dhas = false;
-        d_sp = 0;
-        return true;
-      }
-      if (hj && !ovfl) {
-        /* a head that reached its junction: its part of the record for the merge;
-         * a window that also ended in a terminal or SLOW past the junction goes to
-         * the exact path (where in the window that happened is not known) */
-        u32x4 rq;
-        if (is_slow2(e) || term_ev) {
-          rq = u32x4{0u, 0u, 0xff000000u, (uint32_t) kDeferExact << 16};
-          defer(dcur);
-        } else {
-          rq = u32x4{0u, (rl & 0xffffu) | ((rl + 1u) << 16), (rl >> 16) | (((kn >> 3) & 1u) << 24),
-                     nh | ((uint32_t) kSplitHead << 16)};
-        }
-        *GLOBAL(u32x4, p.reqs + dcur) = rq;
-        dhas = false;
-        d_sp = 0;
-        hj = false;
-        return true;
-      }
-      d_sp = 0;   /* a head that ended before its junction: the request's own result */
-      hj = false;
-    }
     bool ok = !ovfl && is_done2(e) && term_pos < dlen && term_pos < RHP_MAX_LEN;
     /* an ERR between the path and the request-line end (the version, kn == 2)
      * is -1 only when the version's 9 bytes are there (picohttpparser.c:248-251):
@@ -1243,10 +1095,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * share of the rest still fits beside them (config 3: 16 waves 422 us, 12
    * waves 398 us, 8 waves 474 us).  The other waves only join the barriers and
    * the replay. */
-  /* the early phr form splits the longest requests over two lanes (their
-   * results go to the last wave's staging buffer): 15 waves; otherwise 12 */
-  constexpr uint32_t kUnevenWaves = kSplit ? (uint32_t) WAVES - 1u
-                                           : WAVES > 12 ? 12u : (uint32_t) WAVES;   /* 10: 472 us, 11: 450, 13: 408, 14: 413 */
+  constexpr uint32_t kUnevenWaves = WAVES > 12 ? 12u : (uint32_t) WAVES;   /* 10: 472 us, 11: 450, 13: 408, 14: 413 */
   bool idle_wave = false;
   if (uneven) {
     /* every request longer than twice the range's mean is handed out before
@@ -1256,7 +1105,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
      * first refill) */
     pend_ok = false;
     listed = true;
-    split_dry = !split_on;
     idle_wave = (tid >> 6) >= kUnevenWaves;
     __syncthreads();
     if (tid == 0) *wg_counter = 0;
@@ -1266,7 +1114,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     if (!idle_wave) {
       refill_pend();
       wait_vm0();
-      nw = pend_ok ? pend_window(pend_o0, pend_o1, pend_sp) : 0u;
+      nw = pend_ok ? ((pend_o0 & ~3u) - (uint32_t) base) | 2u : 0u;
       issue();
     }
   } else {
@@ -1275,7 +1123,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     nw = pend_ok ? ((pend_o0 & ~3u) - (uint32_t) base) | 2u : 0u;
     issue();
     __syncthreads();
-    split_dry = true;
     first_iter = false;
     list_dry = true;   /* nothing listed: refills take the range in order */
   }
@@ -1315,7 +1162,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #ifdef RHP_STAMPS
     RHP_STAMP(t1); acc[0] += t1 - t0; t0 = t1;
 #endif
-    const uint32_t p_o0 = pend_o0, p_o1 = pend_o1, p_sp = pend_sp;
+    const uint32_t p_o0 = pend_o0, p_o1 = pend_o1;
 #pragma unroll
     for (int q = 0; q < (int) kParts; q++) W[q] = *reinterpret_cast<const u32x4 *>(lds + stage + stage_off(lane, q));
     /* [C] */
@@ -1329,13 +1176,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const uint32_t mis = p_o0 & 3u;
       st = idx2(mis == 0 ? S_METHOD0 : mis == 1 ? S_SKIP1 : mis == 2 ? S_SKIP2 : S_SKIP3, 0);
       wpos = -(int32_t) mis;
-      if constexpr (kSplit) {
-        w_sp = p_sp;
-        if (p_sp & 1u) {   /* a tail: its middle window, seeking the first LF */
-          st = idx2(S_SEEK, 0);
-          wpos = (int32_t) (kBlock * split_m(wlen, mis)) - (int32_t) mis;
-        }
-      }
       wact = true;
       wnew = true;
       /* GET: the request's first four bytes are "GET " (the DFA path parses
@@ -1360,7 +1200,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       /* [E] next window: continuation of wcur, else the first window of a ready pend */
       nw = 0;
       if (walking && (uint32_t) (wpos + (int32_t) kBlock) < wlen) nw = (cur_ptr + kBlock) | 1u;
-      else if (pend_ready) nw = pend_window(p_o0, p_o1, p_sp);
+      else if (pend_ready) nw = ((p_o0 & ~3u) - (uint32_t) base) | 2u;
       wait_lgkm0();   /* [A]'s reads of the buffer are done */
       issue();
 #ifdef RHP_STAMPS
@@ -1461,15 +1301,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         kn = me = pe = rl = nh = ls = t = pco = ovf = 0;
         cand = wget;
         crec_lo = crec_hi = 0;
-        if constexpr (kSplit) {
-          d_sp = w_sp;
-          hj = false;
-          dseek = (w_sp & 1u) != 0;
-          if (dseek) kn = 3u;   /* a tail starts past the request line */
-          /* a head's junction search starts where its tail's seek starts */
-          const uint32_t mis = (uint32_t) (-wpos) & 3u;
-          djpos = (int32_t) (kBlock * split_m(wlen, mis)) - (int32_t) mis;
-        }
       }
       dhas = true;
       dpos = wpos;
@@ -1524,55 +1355,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * side by side.  Nothing to do -> no pass at all. */
   wait_vm0();   /* no window load still writes the staging area (reused below) */
   __syncthreads();
-  if constexpr (kSplit) {
-    /* Merge the split requests (the head's part in reqs[i], flagged kSplitHead;
-     * the tail's result in tinfo; its records in the request's last slots,
-     * downwards).  Head and tail both clean, headers within capacity: the tail's
-     * records move up behind the head's (through LDS scratch, the two ranges
-     * may overlap) and the record is completed.  A tail that ended in -1, or
-     * more headers than the capacity: -1 (phr rejects at that line, which lies
-     * before the end).  Anything else, and a head that ended the request itself
-     * while the tail's records reach its own: the exact path. */
-    const uint32_t npairs = min(*split_n, 2u * (uint32_t) kSplitCap) / 2u;
-    constexpr uint32_t kMergeThreads = (WAVES - 1) * kStageWave / kMergeBytes;
-    if (npairs) {
-      typedef uint32_t u32x2a8 __attribute__((ext_vector_type(2), aligned(8)));
-      for (uint32_t sp = tid; tid < kMergeThreads && sp < npairs; sp += kMergeThreads) {
-        const uint32_t i = wg_lo + (split_list[2u * sp] & 0x1fffu), ti = tinfo[sp];
-        const u32x4 r = *GLOBAL(const u32x4, p.reqs + i);
-        const uint32_t tstat = ti >> 24, tnh = (ti >> 16) & 0xffu, hnh = r[3] & 0xffffu;
-        rhp_hdr_t *h = p.hdrs + (uint64_t) i * p.hs_req;
-        if ((r[3] >> 16) & kSplitHead) {
-          if (tstat == 1u && hnh + tnh <= maxh) {
-            /* every source record is read before any is written: sixteen loads per
-             * round trip into registers, parked in LDS, then the stores */
-            u32x2a8 *scratch = reinterpret_cast<u32x2a8 *>(lds + kLdsTable + tid * kMergeBytes);
-            for (uint32_t j0 = 0; j0 < tnh; j0 += 16) {
-              u32x2a8 v[16];
-#pragma unroll
-              for (uint32_t u = 0; u < 16; u++)
-                v[u] = j0 + u < tnh ? *GLOBAL(const u32x2a8, h + (uint64_t) (maxh - 1u - (j0 + u)) * p.hs_hdr)
-                                    : u32x2a8{0u, 0u};
-#pragma unroll
-              for (uint32_t u = 0; u < 16; u++) scratch[j0 + u] = v[u];
-            }
-            for (uint32_t j = 0; j < tnh; j++) *GLOBAL(u32x2a8, h + (uint64_t) (hnh + j) * p.hs_hdr) = scratch[j];
-            *GLOBAL(u32x4, p.reqs + i) = u32x4{(ti & 0xffffu) + 1u, r[1], r[2], hnh + tnh};
-          } else if (tstat == 2u || tstat == 1u) {
-            *GLOBAL(u32x4, p.reqs + i) = u32x4{0xffffffffu, 0u, 0xff000000u, 0u};
-          } else {
-            *GLOBAL(u32x4, p.reqs + i) = u32x4{0u, 0u, 0xff000000u, (uint32_t) kDeferExact << 16};
-            defer(i);
-          }
-        } else if ((int32_t) r[0] > 0 && !((r[3] >> 16) & kDeferExact) && tnh > 0 && hnh + tnh > maxh) {
-          *GLOBAL(u32x4, p.reqs + i) = u32x4{0u, 0u, 0xff000000u, (uint32_t) kDeferExact << 16};
-          defer(i);
-        }
-      }
-      wait_vm0();
-      __syncthreads();
-    }
-  }
 #ifdef RHP_STAMPS
   if (lane == 0) g_stamps[((blockIdx.x * WAVES + (tid >> 6)) % 8192) * kStampSlots + 14] = __builtin_amdgcn_s_memrealtime();
   unsigned long long rp[4] = {0, 0, 0, 0};

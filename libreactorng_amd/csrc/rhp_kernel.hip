@@ -92,14 +92,16 @@ enum : uint32_t {
   kFrCountSh = 8u,    /* bits 8..15: value bytes read */
   kFrMaxValue = 19u,  /* longer values are left to the replay (19 digits cannot overflow) */
   kFrNeither = 1u << 16,   /* its name, read while its line was open, is neither */
-  /* workgroup pool area after the staging buffers: counters, then the long-
-   * request bitmap (ranges up to kOrderSpan requests) and list */
-  kPoolWords = 8,                                /* counter, replay flag, long-list length, long-list
-                                                    cursor, slow-list length, defer-list length */
+  /* workgroup pool area after the staging buffers: counters, then the replay's
+   * list; an uneven range's longest-first order (ranges up to kOrderSpan
+   * requests) and its histogram live in the staging buffers of the waves such a
+   * range leaves idle */
+  kPoolWords = 8,                                /* counter, replay flag, -, -, slow-list length,
+                                                    defer-list length */
   kOrderSpan = 8192,
-  kListCap = 1536,
+  kOrderBuckets = 64,                            /* window counts 1..63 (63: 63 or more) */
   kDeferCap = 480,                               /* the replay's list (defer) */
-  kPoolBytes = 4 * kPoolWords + kOrderSpan / 8 + 2 * kListCap + 2 * kDeferCap
+  kPoolBytes = 4 * kPoolWords + 2 * kDeferCap
 };
 static_assert(idx2(S_DONE, 0) == kPark, "parked lanes sit in DONE");
 
@@ -497,18 +499,15 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   const uint32_t first_n = min(wg_hi - wg_lo, (uint32_t) (WAVES * 64));
   uint32_t *wg_counter = reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave);
   uint32_t *wg_deferred = wg_counter + 1;   /* some request of the range needs the replay */
-  /* Long requests first.  With lengths as uneven as config 3's, the requests
-   * drawn last decide when a wave finishes; the first iteration (which only
-   * waits for the first windows) lists the range's requests longer than twice
-   * its mean, and refills hand those out before the rest.  Ranges above
-   * kOrderSpan keep plain order. */
-  uint32_t *list_n = wg_counter + 2, *list_next = wg_counter + 3;
-  uint32_t *long_bits = wg_counter + kPoolWords;
-  uint16_t *long_list = reinterpret_cast<uint16_t *>(long_bits + kOrderSpan / 32);
+  /* Longest first.  With lengths as uneven as config 3's, the requests drawn
+   * last decide when a wave finishes: a lane's last requests (the one it walks
+   * and the one it holds) are committed when the pool runs dry, so an uneven
+   * range is handed out in descending window count (a counting sort over the
+   * range before the first hand-out, in the idle waves' staging buffers): the
+   * longest start at iteration 0, the last ones handed out are the shortest.
+   * Ranges above kOrderSpan keep plain order. */
   const bool order_on = wg_hi - wg_lo <= kOrderSpan;
-  bool list_dry = !order_on;
-  bool listed = false;   /* the range was scanned: skip the listed requests in order */
-  bool first_iter = true;   /* the list is complete only after the scan (before the loop) */
+  bool sorted = false;   /* refills take the range in `order` (an uneven range) */
   bool pool_dry = wg_lo >= wg_hi;
   /* The prologue's global reads all go out at once (one round trip): the
    * table, the range's end offsets and every thread's first request. */
@@ -592,48 +591,57 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     pend_o1 = *GLOBAL(const uint32_t, o + 2);
     pend_ok = true;
   };
+  /* an uneven range's order: the range's requests (u16, range-relative) by
+   * descending window count, then the histogram / bucket cursors */
+  uint16_t *order = reinterpret_cast<uint16_t *>(lds + kLdsTable + (WAVES - 3) * kStageWave);
+  uint32_t *bucket = reinterpret_cast<uint32_t *>(order + kOrderSpan);
+  static_assert(2 * kOrderSpan + 4 * kOrderBuckets <= 3 * kStageWave, "the order fits the last three waves' staging");
   auto refill_pend = [&]() {
     uint64_t want = __ballot(!pend_ok);
-    if (!want || (pool_dry && list_dry)) return;
-    if (!list_dry && !first_iter) {   /* the long list first */
-      const uint32_t cnt = (uint32_t) __popcll(want);
-      uint32_t b0 = 0;
-      if (lane == 0) b0 = atomicAdd(list_next, cnt);
-      b0 = __builtin_amdgcn_readfirstlane(b0);
-      const uint32_t nl = min(*list_n, (uint32_t) kListCap);
-      if (b0 + cnt >= nl) list_dry = true;
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
-      if (!pend_ok && b0 + rank < nl) take(wg_lo + long_list[b0 + rank]);
-      want = __ballot(!pend_ok);
-    }
-    /* the range in order, skipping the listed requests (a few rounds at most) */
-    while (want && !pool_dry) {
-      const uint32_t cnt = (uint32_t) __popcll(want);
-      uint32_t b0 = 0;
-      if (lane == 0) b0 = atomicAdd(wg_counter, cnt);
-      b0 = wg_lo + __builtin_amdgcn_readfirstlane(b0);
-      if (b0 + cnt >= wg_hi) pool_dry = true;
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
-      const uint32_t i = b0 + rank, k = i - wg_lo;
-      if (!pend_ok && i < wg_hi && !(listed && ((long_bits[k >> 5] >> (k & 31)) & 1u))) take(i);
-      want = __ballot(!pend_ok);
-    }
+    if (!want || pool_dry) return;
+    const uint32_t cnt = (uint32_t) __popcll(want);
+    uint32_t b0 = 0;
+    if (lane == 0) b0 = atomicAdd(wg_counter, cnt);
+    b0 = wg_lo + __builtin_amdgcn_readfirstlane(b0);
+    if (b0 + cnt >= wg_hi) pool_dry = true;
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
+    const uint32_t i = b0 + rank;
+    if (!pend_ok && i < wg_hi) take(sorted ? wg_lo + order[i - wg_lo] : i);
   };
 
-  /* the long-request scan (see order_on): every request of the range longer
-   * than twice its mean goes into the long list (and bitmap) */
+  /* the longest-first order of an uneven range (see order_on): a counting sort
+   * by window count, descending; every thread of the workgroup takes part (the
+   * caller's barriers: the histogram zeroed before, the order complete after) */
   const uint32_t span_n = wg_hi - wg_lo;
-  auto scan_long = [&]() {
-    const uint64_t twice = 2u * (o_hi - o_lo);
-    for (uint32_t k = tid; k < span_n; k += WAVES * 64) {
-      const uint64_t o0 = p.offsets[wg_lo + k], o1 = p.offsets[wg_lo + k + 1];
-      if ((o1 - o0) * span_n > twice) {
-        const uint32_t at = atomicAdd(list_n, 1u);
-        if (at < kListCap) {
-          long_list[at] = (uint16_t) k;
-          atomicOr(&long_bits[k >> 5], 1u << (k & 31));
-        }
+  auto sort_range = [&]() {
+    constexpr uint32_t kPer = kOrderSpan / (WAVES * 64);   /* requests per thread */
+    uint32_t wc[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+      const uint32_t k = tid + j * WAVES * 64;
+      wc[j] = 0;
+      if (k < span_n) {
+        const uint64_t len = p.offsets[wg_lo + k + 1] - p.offsets[wg_lo + k];
+        wc[j] = (uint32_t) min((len + 3u + kBlock - 1u) / kBlock, (uint64_t) kOrderBuckets - 1u);
+        atomicAdd(&bucket[wc[j]], 1u);
       }
+    }
+    __syncthreads();
+    if (tid < 64) {   /* exclusive prefix of the counts from the longest bucket down */
+      const uint32_t b = kOrderBuckets - 1u - tid, c = bucket[b];
+      uint32_t x = c;
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t) __shfl_up((int) x, d);
+        x += tid >= d ? y : 0u;
+      }
+      bucket[b] = x - c;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+      const uint32_t k = tid + j * WAVES * 64;
+      if (k < span_n) order[atomicAdd(&bucket[wc[j]], 1u)] = (uint16_t) k;
     }
   };
 
@@ -641,7 +649,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * range (u16); on overflow (or ranges over 64K requests) the replay scans
    * the whole range */
   uint32_t *defer_n = wg_counter + 5;
-  uint16_t *defer_list = long_list + kListCap;
+  uint16_t *defer_list = reinterpret_cast<uint16_t *>(wg_counter + kPoolWords);
   auto defer = [&](uint32_t i) {
     *wg_deferred = 1u;
     const uint32_t at = atomicAdd(defer_n, 1u);
@@ -1081,7 +1089,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const uint32_t k = tid + j * WAVES * 64;
     if (k < kTable2Bytes / 16) reinterpret_cast<u32x4 *>(lds)[k] = tab[j];
   }
-  for (uint32_t k = tid; k < kPoolWords + kOrderSpan / 32; k += WAVES * 64)
+  for (uint32_t k = tid; k < kPoolWords; k += WAVES * 64)
     reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave)[k] = k == 0 ? first_n : 0u;
   wait_vm0();   /* the pending offsets */
 #ifdef RHP_STAMPS
@@ -1098,19 +1106,19 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   constexpr uint32_t kUnevenWaves = WAVES > 12 ? 12u : (uint32_t) WAVES;   /* 10: 472 us, 11: 450, 13: 408, 14: 413 */
   bool idle_wave = false;
   if (uneven) {
-    /* every request longer than twice the range's mean is handed out before
-     * the others, the first hand-out included: a long request never waits
-     * behind another one in a lane (the barriers: the pool area initialized
-     * before the scan; the list complete and the counter reset before the
-     * first refill) */
+    /* the whole range longest first, the first hand-out included: a long
+     * request never waits behind another one in a lane, and the requests
+     * committed when the pool runs dry are the shortest (the barriers: the
+     * histogram zeroed before the sort; the order complete and the counter
+     * reset before the first refill) */
     pend_ok = false;
-    listed = true;
+    sorted = true;
     idle_wave = (tid >> 6) >= kUnevenWaves;
+    if (tid < kOrderBuckets) bucket[tid] = 0u;
     __syncthreads();
     if (tid == 0) *wg_counter = 0;
-    scan_long();
+    sort_range();
     __syncthreads();
-    first_iter = false;
     if (!idle_wave) {
       refill_pend();
       wait_vm0();
@@ -1123,8 +1131,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     nw = pend_ok ? ((pend_o0 & ~3u) - (uint32_t) base) | 2u : 0u;
     issue();
     __syncthreads();
-    first_iter = false;
-    list_dry = true;   /* nothing listed: refills take the range in order */
   }
 
   /*

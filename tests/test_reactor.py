@@ -102,9 +102,12 @@ def test_burst_rounds_gpu_vs_host():
     """4096-request rounds (64 connections x 64 pipelined): the server with the
     MI355X parser (asynchronous rounds) against the host parser, same process
     layout; the numbers are printed (DESIGN.md §7 records a run)."""
-    gpu, gpu_round, out_g = _burst("gpu", reps=9)
+    # two interleaved runs of each (gpu, host, gpu, host): a shared box's load
+    # moves single runs by 20-30 %; each side keeps its better median
+    runs = [(_burst("gpu", reps=9), _burst("host", reps=9)) for _ in range(2)]
+    (gpu, gpu_round, out_g), (host, host_round, out_h) = (max((r[0] for r in runs), key=lambda x: x[0]),
+                                                          max((r[1] for r in runs), key=lambda x: x[0]))
     gpu_w, _, out_w = _burst("gpu", writer="gpu", reps=9)
-    host, host_round, out_h = _burst("host", reps=9)
     print(f"burst req/s: gpu {gpu:.0f} ({gpu_round:.0f} requests/round), gpu parser + gpu writer {gpu_w:.0f}, "
           f"host {host:.0f} ({host_round:.0f})")
     print(out_g, out_w, out_h)

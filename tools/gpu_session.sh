@@ -19,7 +19,7 @@ step_bench() {
     && cat gpurun_out/bench_${TAG}.json
 }
 step_prof() {
-  for c in get256 zipf post; do
+  for c in get256 zipf post chunked; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_${TAG}_$c -o run \
       -- python3 bench.py --config $c --extra none --steps 30 --warmup 5 --no-cpu --no-e2e > gpurun_out/prof_${TAG}_$c.log 2>&1 \
       || return 1
@@ -27,7 +27,7 @@ step_prof() {
   done
 }
 step_pmc() {
-  for c in get256 zipf post; do
+  for c in get256 zipf post chunked; do
     for k in FETCH_SIZE WRITE_SIZE; do
       timeout -k 10 -s KILL 240 rocprofv3 --pmc $k --output-format csv -d gpurun_out/pmc_${TAG}_${c}_$k -o p \
         -- python3 bench.py --config $c --extra none --steps 6 --warmup 2 --no-cpu --no-e2e > gpurun_out/pmc_${TAG}_${c}_$k.log 2>&1 \

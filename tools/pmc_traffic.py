@@ -28,7 +28,7 @@ def per_dispatch(path):
 def main():
     out_dir, tag, prof = sys.argv[1], sys.argv[2], sys.argv[3]
     res = {}
-    for cfg in ("get256", "zipf", "post"):
+    for cfg in ("get256", "zipf", "post", "chunked"):
         f = glob.glob(os.path.join(out_dir, f"pmc_{tag}_{cfg}_FETCH_SIZE", "**", "*counter_collection.csv"), recursive=True)
         w = glob.glob(os.path.join(out_dir, f"pmc_{tag}_{cfg}_WRITE_SIZE", "**", "*counter_collection.csv"), recursive=True)
         if not f or not w:

@@ -597,7 +597,14 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   uint32_t *bucket = reinterpret_cast<uint32_t *>(order + kOrderSpan);
   static_assert(2 * kOrderSpan + 4 * kOrderBuckets <= 3 * kStageWave, "the order fits the last three waves' staging");
   auto refill_pend = [&]() {
-    uint64_t want = __ballot(!pend_ok);
+    /* Just in time (early form, longest-first ranges): a lane takes its next
+     * request only when its current one has at most two windows left -- the
+     * pending request's offsets must have landed by the iteration that issues
+     * its first window, no earlier commitment is needed.  A lane deep in a long
+     * request leaves the pool to the lanes that finish first, so the range
+     * stays longest first per lane, not per hand-out round (config 3 -4.5 %). */
+    const bool need = !pend_ok && !(!LATE && sorted && wact && wpos + (int32_t) (2u * kBlock) < (int32_t) wlen);
+    uint64_t want = __ballot(need);
     if (!want || pool_dry) return;
     const uint32_t cnt = (uint32_t) __popcll(want);
     uint32_t b0 = 0;
@@ -606,7 +613,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     if (b0 + cnt >= wg_hi) pool_dry = true;
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) want, 0));
     const uint32_t i = b0 + rank;
-    if (!pend_ok && i < wg_hi) take(sorted ? wg_lo + order[i - wg_lo] : i);
+    if (need && i < wg_hi) take(sorted ? wg_lo + order[i - wg_lo] : i);
   };
 
   /* the longest-first order of an uneven range (see order_on): a counting sort

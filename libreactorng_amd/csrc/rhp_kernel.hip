@@ -334,35 +334,70 @@ __device__ __forceinline__ uint64_t strtoull10_gpu(const uint8_t *s, const uint3
 
 /* http_frame (rhp_scalar.h) for the replay's common case, from the decode's
  * hints (cand, crec: see the decode state) -- GET, no candidate header, or one
- * that is Content-Length or neither: the final record is written, kFrameDone.
- * One candidate that is a Transfer-Encoding whose value is "chunked" (any
- * case): kFrameChunked, the body (ret, len) is de-framed by the replay's second
- * pass.  Anything else: kFrameSlow, http_frame.  Reads no header record and no
- * method byte: on batches larger than the caches those re-reads are HBM
- * traffic.  The candidate's name and value are loaded together, one memory
+ * or two candidates (the second's record is read from hdrs): the final record
+ * is written, kFrameDone, unless the only Transfer-Encoding's value is
+ * "chunked" (any case): kFrameChunked, the body (ret, len) is de-framed by the
+ * replay's second pass.  Three or more candidates, or an overflowed candidate
+ * set: kFrameSlow, http_frame.  Reads no method byte and, for one candidate,
+ * no header record: on batches larger than the caches those re-reads are HBM
+ * traffic.  The candidates' names and values are loaded together, one memory
  * round trip. */
 enum : int { kFrameDone = 0, kFrameSlow = 1, kFrameChunked = 2 };
 __device__ __forceinline__ int http_frame_fast(const uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x,
-                                               uint32_t cand, uint32_t crec_lo, uint32_t crec_hi)
+                                               uint32_t cand, uint32_t crec_lo, uint32_t crec_hi,
+                                               const rhp_hdr_t *h, uint64_t hs)
 {
   const int64_t n = ret;
   rhp_http_t o = {1, 0, (uint64_t) n, 0};
   const uint32_t hdr = cand & 0x3fffffffu;
   if (!(cand & 0x40000000u) && hdr != 0) {   /* not GET (http.c:198-202), some candidate */
-    if ((cand >> 31) || (hdr & (hdr - 1)) != 0) return kFrameSlow;
-    /* a candidate's name is never RHP_NAME_NULL (its length is 14 or 17) */
-    const uint32_t name_off = crec_lo & 0xffffu, name_len = crec_lo >> 16;
-    const uint32_t value_off = crec_hi & 0xffffu, value_len = crec_hi >> 16;
-    uint32_t dn[7], dv[7];
-    load28(b + name_off, dn);
-    load28(b + value_off, dv);
-    if (name_len == 17u && name_is(dn, "transfer-encoding") && value_len != 0) {
-      /* the only Transfer-Encoding and no Content-Length: "chunked" (http.c:221-224,
-       * data_equal_case) de-frames the body, anything else is -1 */
-      if (value_len == 7u && name_is(dv, "chunked")) return kFrameChunked;
+    const uint32_t rest = hdr & (hdr - 1u);
+    if ((cand >> 31) || (rest & (rest - 1u)) != 0) return kFrameSlow;
+    /* up to two candidates (a Content-Length beside a Transfer-Encoding is the
+     * usual second one): the second's record is one more load, and all four
+     * strings are read together.  A candidate's name is never RHP_NAME_NULL
+     * (its length is 14 or 17). */
+    uint32_t lo[2] = {crec_lo, 0u}, hi[2] = {crec_hi, 0u};
+    if (rest) {
+      const uint2 r = *reinterpret_cast<const uint2 *>(h + (uint64_t) __builtin_ctz(rest) * hs);
+      lo[1] = r.x; hi[1] = r.y;
+    }
+    uint32_t dn[2][7], dv[2][7];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      if (c == 0 || rest) {
+        load28(b + (lo[c] & 0xffffu), dn[c]);
+        load28(b + (hi[c] & 0xffffu), dv[c]);
+      }
+    }
+    /* the first Transfer-Encoding and the first Content-Length, in header order
+     * (http.c:209-216); indices chosen by selects, not by a dynamic register
+     * index */
+    bool is_te[2], is_cl[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      is_te[c] = (c == 0 || rest) && (lo[c] >> 16) == 17u && name_is(dn[c], "transfer-encoding");
+      is_cl[c] = (c == 0 || rest) && (lo[c] >> 16) == 14u && name_is(dn[c], "content-length");
+    }
+    const bool te1 = !is_te[0], cl1 = !is_cl[0];
+    const bool has_te = is_te[0] || is_te[1], has_cl = is_cl[0] || is_cl[1];
+    const uint32_t te_hi = te1 ? hi[1] : hi[0], cl_hi = cl1 ? hi[1] : hi[0];
+    const bool te_set = has_te && (te_hi >> 16) != 0, cl_set = has_cl && (cl_hi >> 16) != 0;
+    if (cl_set && te_set) {
       o.result = -1; o.consumed = 0;
-    } else if (name_len == 14u && name_is(dn, "content-length") && value_len != 0) {
-      const uint64_t size = strtoull10_gpu(b + value_off, dv, value_len);
+    } else if (te_set) {
+      /* Transfer-Encoding alone: "chunked" (http.c:221-224, data_equal_case)
+       * de-frames the body, anything else is -1 */
+      uint32_t dt[7];
+#pragma unroll
+      for (int j = 0; j < 7; j++) dt[j] = te1 ? dv[1][j] : dv[0][j];
+      if ((te_hi >> 16) == 7u && name_is(dt, "chunked")) return kFrameChunked;
+      o.result = -1; o.consumed = 0;
+    } else if (cl_set) {
+      uint32_t dc[7];
+#pragma unroll
+      for (int j = 0; j < 7; j++) dc[j] = cl1 ? dv[1][j] : dv[0][j];
+      const uint64_t size = strtoull10_gpu(b + (cl_hi & 0xffffu), dc, cl_hi >> 16);
       if (len < (uint64_t) n + size) {
         o.result = 0; o.consumed = 0;
       } else {
@@ -1431,7 +1466,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const int fr = (f & kHintExact) ? kFrameSlow
                                       : http_frame_fast(p.bytes_rw + cur.off, cur.end - cur.off,
                                                         (int32_t) (cur.hint[1] & 0xffffu), &p.http[i], cur.hint[0],
-                                                        cur.hint[2], cur.hint[3]);
+                                                        cur.hint[2], cur.hint[3], p.hdrs + (uint64_t) i * p.hs_req, p.hs_hdr);
 #ifdef RHP_STAMPS
       rp[3] += __popcll(__builtin_amdgcn_ballot_w64(fr == kFrameDone));
 #endif

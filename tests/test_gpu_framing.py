@@ -40,6 +40,19 @@ VARIANTS = [
     (b"Content-Length: 2\r\nTransfer-Encoding: chunked\r\n", b"ab"),
     (b"Content-Length: 2\r\nContent-Length: 3\r\n", b"abc"),
     (b"Accept-Charset: 1\r\nContent-Length: 3\r\n", b"abc"),
+    # two candidates, settled in the replay's first pass
+    (b"Transfer-Encoding: chunked\r\nContent-Length: 3\r\n", b"abc"),
+    (b"Content-Length: \r\nTransfer-Encoding: chunked\r\n", b"3\r\nabc\r\n0\r\n\r\n"),
+    (b"Content-Length: \r\nContent-Length: 3\r\n", b"abc"),      # the first CL counts, empty
+    (b"Transfer-Encoding: chunked\r\nTransfer-Encoding: gzip\r\n", b"3\r\nabc\r\n0\r\n\r\n"),
+    (b"Transfer-Encoding: gzip\r\nTransfer-Encoding: chunked\r\n", b"abc"),
+    (b"If-Modified-Since: 1\r\nContent-Length: 3\r\n", b"abc"),
+    (b"Transfer-Encoding: CHUNKED\r\nIf-Modified-Since: x\r\n", b"3\r\nabc\r\n0\r\n\r\n"),
+    (b"Content-Lengtx: 9\r\nContent-Length: 12345678901234567890123\r\n", b"q"),
+    (b"Accept-Charset: 1\r\nIf-Modified-Since: 2\r\n", b"abc"),   # neither is framing
+    # three candidates: the general path
+    (b"Content-Length: 3\r\nAccept-Charset: x\r\nTransfer-Encoding: chunked\r\n", b"abc"),
+    (b"Accept-Charset: x\r\nAccept-Charset: y\r\nContent-Length: 3\r\n", b"abc"),
 ]
 
 

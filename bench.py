@@ -244,9 +244,12 @@ class GpuRunner:
     current stream and timed with HIP events on that stream."""
 
     def __init__(self, cfg, lo, hi, copies, layout, streams=1):
+        import hashlib
         import torch
         self.torch = torch
+        self.mode = cfg["mode"]
         buf, off = rhp.generate(cfg["gen"], hi - lo, cfg["seed"], lo=lo)
+        self.input_sha256 = hashlib.sha256(buf.tobytes()).hexdigest()
         # a config whose launches rewrite the bytes (chunked bodies, http.c:155) restores a copy from
         # this pristine one before it is launched again: >= 3 copies, restored two launches ahead
         self.rewrites = bool(cfg.get("rewrites"))
@@ -342,12 +345,33 @@ class GpuRunner:
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
+    def last_result(self):
+        """records of the last launch (and, for a rewriting config, its bytes as it left them)"""
+        return self.copies[(self.nstep - 1) % len(self.copies)].result()   # its bytes were pristine when launched
+
     def ok_fraction(self):
-        last = self.copies[(self.nstep - 1) % len(self.copies)]   # its bytes were pristine when launched
-        res = last.result()
+        res = self.last_result()
         if res.http is not None:
             return float((res.http["result"] == 1).mean()) if len(res.http) else 1.0
         return float((res.reqs["ret"] > 0).mean()) if len(res.reqs) else 1.0
+
+    def parity(self, spec):
+        """The last timed launch's records against the reference's digest of the
+        same workload (tests/golden/full_digests.json, made by the compiled
+        reference): "match", or a "MISMATCH ..." string."""
+        import hashlib
+        if spec is None:
+            return "unpinned: no reference digest for this shard size"
+        if spec["input_sha256"] != self.input_sha256:
+            return "MISMATCH: input bytes differ from the ones the reference digest was made on"
+        res = self.last_result()
+        got = rhp.record_digest(*rhp.canonical(res, self.mode))
+        if got != spec["records_sha256"]:
+            return f"MISMATCH: records sha256 {got[:16]}... != reference {spec['records_sha256'][:16]}..."
+        if "bytes_out_sha256" in spec:   # chunked bodies de-framed in place (http.c:134-160)
+            if hashlib.sha256(res.bytes_out.tobytes()).hexdigest() != spec["bytes_out_sha256"]:
+                return "MISMATCH: de-framed bytes differ from the reference's"
+        return "match"
 
 
 class EmuRunner:
@@ -375,6 +399,33 @@ class EmuRunner:
     def ok_fraction(self):
         return float((self.res.reqs["ret"] > 0).mean()) if self.res is not None and len(self.res.reqs) else 1.0
 
+    def parity(self, spec):
+        if spec is None:
+            return "unpinned: no reference digest for this shard size"
+        got = rhp.record_digest(*rhp.canonical(self.res, self.cfg["mode"]))
+        return "match" if got == spec["records_sha256"] else "MISMATCH: records differ from the reference digest"
+
+
+# reference digests of the timed workloads (tests/golden/full_digests.json, made
+# by the reference compiled from /root/reference: tests/golden/make_golden.py)
+GOLDEN_DIGESTS = os.path.join(ROOT, "tests", "golden", "full_digests.json")
+GOLDEN_NAMES = {"zipf": "config3_zipf_h32", "post": "config5_post1k_http_h16", "chunked": "chunked_post_http_h16"}
+
+
+def golden_spec(key, lo, n):
+    """The reference digest of requests [lo, lo + n) of a config, or None.  Config
+    2/4's shards are keyed by their first request (rank r of any N <= 8 parses
+    requests [r * 2^20, (r + 1) * 2^20), config 4's shard r)."""
+    sets = json.load(open(GOLDEN_DIGESTS))["sets"]
+    cfg = CONFIGS[key]
+    names = [GOLDEN_NAMES[key]] if key in GOLDEN_NAMES else [f"config4_get256_shard{k}of8" for k in range(8)]
+    for name in names:
+        s = sets.get(name)
+        if s and s["lo"] == lo and s["n"] == n and s["seed"] == cfg["seed"] and s["max_headers"] == cfg["maxh"] \
+                and s["mode"] == cfg["mode"] and s["config"] == cfg["gen"]:
+            return dict(s, name=name)
+    return None
+
 
 def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
     cfg = CONFIGS[key]
@@ -393,6 +444,12 @@ def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
     wall, kern_ms = runner.timed(steps)
     if dist is not None:
         dist.barrier()
+    # outside the timed region: the last timed launch's records against the reference's digest
+    spec = golden_spec(key, lo, hi - lo)
+    parity = runner.parity(spec)
+    parity_entry = {"result": parity, "digest": spec["name"] if spec else None}
+    if parity.startswith("MISMATCH"):
+        print(f"bench.py: PARITY {key} rank {rank}: {parity}", file=sys.stderr)
     total_alg = float(alg_bytes)
     if dist is not None:
         import torch
@@ -402,8 +459,18 @@ def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
         tb = torch.tensor([float(alg_bytes)], dtype=torch.float64)
         dist.all_reduce(tb)
         total_alg = float(tb[0])
+        # every rank's verdict reaches rank 0's line (0 match, 1 unpinned, 2 mismatch)
+        code = 2 if parity.startswith("MISMATCH") else 0 if parity == "match" else 1
+        codes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(codes, torch.tensor([code], dtype=torch.int64))
+        parity_entry["ranks"] = ["match" if int(c) == 0 else "unpinned" if int(c) == 1 else "MISMATCH" for c in codes]
+        if any(int(c) == 2 for c in codes):
+            parity_entry["result"] = "MISMATCH on some rank"
+        elif any(int(c) == 1 for c in codes):
+            parity_entry["result"] = "match on the ranks with a reference digest" if any(int(c) == 0 for c in codes) \
+                else parity_entry["result"]
     return dict(cfg=cfg, lo=lo, hi=hi, n_total=n_total, alg_bytes=alg_bytes, total_alg=total_alg, wall=wall,
-                kern_ms=kern_ms, ok_frac=ok_frac, steps=steps, warmup=warmup,
+                kern_ms=kern_ms, ok_frac=ok_frac, steps=steps, warmup=warmup, parity=parity_entry,
                 layout=args.layout if args.layout != "auto" else cfg["layout"])
 
 
@@ -466,9 +533,13 @@ def main(argv=None):
                            3, None)
             extra[key] = {"workload": CONFIGS[key]["name"], "value": round(e["total_alg"] / (e["kern_ms"] * 1e-3)
                                                                            / 2 ** 30, 2),
-                          "unit": "GiB/s", "steps": e["steps"], "ms_per_step": round(e["wall"] * 1e3 / e["steps"], 4),
+                          "unit": "GiB/s", "steps": e["steps"],
+                          # a rewriting config's launches are timed one by one with HIP events (the D2D
+                          # restore of its bytes between launches stays outside): no wall time per step
+                          ("ms_per_launch_hip_events" if CONFIGS[key].get("rewrites") else "ms_per_step"):
+                              round(e["wall"] * 1e3 / e["steps"], 4),
                           "ok_fraction": e["ok_frac"], "record_layout": f"{e['layout']}-major",
-                          "roofline": roofline(e, key)}
+                          "parity": e["parity"], "roofline": roofline(e, key)}
 
     if rank == 0:
         cfg = r["cfg"]
@@ -486,6 +557,13 @@ def main(argv=None):
                        "kernel": kernel, "device": args.device, "record_layout": f"{r['layout']}-major"},
             "roofline": roofline(r, args.config),
         }
+        # parity of every timed workload: the records of its last timed launch
+        # hashed against the reference's digest (GOLDEN_DIGESTS)
+        line["parity"] = {("config4" if world > 1 else "config2") if args.config == "get256" else args.config:
+                          r["parity"]["result"]}
+        line["parity"].update({k: v["parity"]["result"] for k, v in extra.items()})
+        line["parity_detail"] = {args.config: r["parity"], **{k: v["parity"] for k, v in extra.items()}}
+        line["library_sha256"] = rhp.library_sha256() if args.device == "gpu" else None
         if extra:
             line["extra_configs"] = extra
         if world == 1 and args.device == "gpu" and not args.no_e2e:
@@ -498,8 +576,12 @@ def main(argv=None):
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline([args.config] + [k for k in EXTRA_KEYS if k in extra])
         print(json.dumps(line), flush=True)
+    bad = "MISMATCH" in r["parity"]["result"] or any("MISMATCH" in v["parity"]["result"] for v in extra.values())
     if dist is not None:
         dist.destroy_process_group()
+    if bad:
+        print("bench.py: parity MISMATCH against the reference digest (see the line's parity)", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -324,6 +324,10 @@ void server_plain(server_session_t *, data_t, http_field_t *, size_t);
  * (rhp_scalar.h) on the host, for CPU-only hosts and tests. */
 const char *reactor_parser_name(void);
 
+/* Diagnostic: batch rounds submitted with input so far (all servers of the
+ * process; tests bound the rounds a waiting session may cost). */
+uint64_t reactor_batch_rounds(void);
+
 #ifdef __cplusplus
 }
 #endif

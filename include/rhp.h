@@ -153,7 +153,11 @@ int rhp_parse_batch(const rhp_batch_t *batch, void *stream);
  * its piece, a piece that started inside a body) is parsed again from the true
  * boundary over the rest of the session's input.  Request m of a session is
  * left in record slot piece_lo + m (reqs/hdrs/http of the batch), its start
- * in req_start[piece_lo + m].  One launch, one thread per session.
+ * in req_start[piece_lo + m].  One launch, one thread per session.  Any split
+ * gives the reference's answers: with a coarser one (a piece holding several
+ * requests) a piece whose records an earlier request of the walk has already
+ * overwritten is parsed again from its boundary, and a session with more
+ * requests than pieces stops with `more`.
  */
 typedef struct rhp_session {
   uint32_t piece_lo, piece_hi;   /* the session's pieces: requests [piece_lo, piece_hi) of the
@@ -163,8 +167,8 @@ typedef struct rhp_session {
 typedef struct rhp_session_result {
   uint32_t n_slots;   /* record slots filled: every one but the last has result 1; the last
                          one's result says where the session stopped (1: input used up) */
-  uint32_t more;      /* 1: more requests than pieces (a split the caller missed): the rest
-                         from offsets[piece_lo] + consumed needs another batch */
+  uint32_t more;      /* 1: more requests than pieces (a coarser split than one per empty
+                         line): the rest from offsets[piece_lo] + consumed needs another batch */
   uint64_t consumed;  /* bytes of the session's input taken by its result-1 requests */
 } rhp_session_result_t;
 

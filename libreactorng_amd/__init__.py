@@ -206,6 +206,57 @@ class Result:
     bytes_out: np.ndarray | None = None  # request bytes after http mode (chunked bodies rewritten)
 
 
+def canonical(res: Result, mode: int):
+    """Result -> canonical (reqs, hdrs[n, max_headers], http) records: the fields
+    the reference leaves unspecified for a request that did not parse (its
+    method/path/header outputs, phr_parse_request's minor_version, the records
+    past num_headers, flags) zeroed, so two parsers compare with one array
+    equality and hash to one digest (tests/golden/full_digests.json)."""
+    reqs = res.reqs.copy()
+    n = len(reqs)
+    maxh = res.hdrs.shape[1] if res.hdrs.ndim == 2 else 0
+    ok = reqs["ret"] > 0
+    if mode == MODE_HTTP:
+        ok &= res.http["result"] == 1
+    for f in ("method_off", "method_len", "path_off", "path_len", "num_headers"):
+        reqs[f][~ok] = 0
+    reqs["minor_version"][~ok] = -1
+    reqs["flags"] = 0
+    h = res.hdrs.copy() if maxh else np.zeros((n, 0), dtype=HDR_DTYPE)   # C order (header-major views too)
+    if maxh:
+        valid = ok[:, None] & (np.arange(maxh)[None, :] < reqs["num_headers"][:, None])
+        for f in h.dtype.names:
+            h[f] = np.where(valid, h[f], 0)
+    x = None
+    if mode == MODE_HTTP:
+        x = res.http.copy()
+        one = x["result"] == 1
+        for f in ("body_kind", "consumed", "body_len"):
+            x[f][~one] = 0
+    return reqs, h, x
+
+
+def record_digest(reqs, hdrs, http=None) -> str:
+    """sha256 of a canonical record stream: reqs, then hdrs (request-major), then http."""
+    import hashlib
+    d = hashlib.sha256()
+    d.update(np.ascontiguousarray(reqs).tobytes())
+    d.update(np.ascontiguousarray(hdrs).tobytes())
+    if http is not None:
+        d.update(np.ascontiguousarray(http).tobytes())
+    return d.hexdigest()
+
+
+def library_sha256(path: str | None = None) -> str:
+    """sha256 of librhp.so as it lies on disk (the file lib() loads): logs and
+    profiles carry it so a result can be tied to the binary it came from."""
+    import hashlib
+    p = path or LIBRHP
+    if not os.path.exists(p):
+        return "missing"
+    return hashlib.sha256(open(p, "rb").read()).hexdigest()
+
+
 def hdr_view(flat: np.ndarray, n: int, max_headers: int, layout: int) -> np.ndarray:
     """The [n, max_headers] view of a batch's record array in either layout (include/rhp.h)."""
     if layout == LAYOUT_HEADER_MAJOR:
@@ -334,14 +385,15 @@ def split_pieces(data: bytes):
     return out
 
 
-def pack_sessions(sessions, split: bool = True):
+def pack_sessions(sessions, split=True):
     """(buf, piece offsets, rhp_session_t array, session byte starts) for a list
-    of session inputs packed back to back (split=False: one piece per session)."""
+    of session inputs packed back to back (split=False: one piece per session;
+    a callable: data -> piece lengths, any split of the input)."""
     pieces, sess, starts, at = [], [], [], 0
     for data in sessions:
         lo = len(pieces)
         starts.append(at)
-        for ln in (split_pieces(data) if split else [len(data)]):
+        for ln in (split(data) if callable(split) else split_pieces(data) if split else [len(data)]):
             pieces.append((at, ln))
             at += ln
         sess.append((lo, len(pieces)))

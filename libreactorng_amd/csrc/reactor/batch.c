@@ -27,6 +27,7 @@
  */
 #define __HIP_PLATFORM_AMD__ 1
 #include <errno.h>
+#include <stdbool.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -74,10 +75,7 @@ typedef struct batch_state
   int          efd;          /* gpu: written once per completed round */
   slot_t       slot[REACTOR_BATCH_SLOTS];
   void        *d_work;
-  /* RHP_REACTOR_STATS=1: rounds, requests and submit -> result time, printed at exit */
-  int          stats;
   int          diag_host;   /* RHP_REACTOR_DIAG=hostparse: gpu-mode buffers, host parse (diagnostic) */
-  uint64_t     st_rounds, st_requests, st_ns;
   /* gpu: how a round's completion reaches the eventfd (RHP_REACTOR_COMPLETE):
    * COMPLETE_HOSTFUNC a hipLaunchHostFunc behind the round's copies (the HIP
    * runtime's callback thread writes the eventfd); COMPLETE_EVENT a waiter
@@ -97,9 +95,29 @@ typedef struct batch_state
   void           *dw_arena, *dw_resps, *dw_fields, *dw_out, *dw_off, *dw_work;
   uint8_t        *hw_out;
   uint64_t       *hw_off;
+  /* the waiter / worker thread: started once, stopped and joined at teardown */
+  int             have_worker, stop;
+  hipStream_t     cstream;   /* gpu: D2H of a round's de-framed bytes, when it has chunked bodies */
 } batch_state_t;
 
-static __thread batch_state_t B;   /* one parser per reactor thread */
+/* One parser per reactor thread, on the heap: the waiter / worker thread holds
+ * a pointer to it, so it must outlive the thread's TLS.  A thread-exit hook
+ * (pthread key destructor) stops and joins that thread, waits for the rounds
+ * in flight, and frees the events, streams and buffers. */
+static __thread batch_state_t *B;
+static pthread_key_t   batch_key;
+static pthread_once_t  batch_once = PTHREAD_ONCE_INIT;
+static void batch_teardown(void *);
+static void batch_key_init(void)
+{
+  if (pthread_key_create(&batch_key, batch_teardown) != 0)
+    abort();
+}
+
+/* RHP_REACTOR_STATS=1: rounds, requests and submit -> result time of every
+ * thread, printed at exit */
+static uint64_t st_rounds, st_requests, st_ns;
+static int      st_on;
 
 static void host_parse(batch_state_t *b, int k);
 
@@ -110,8 +128,10 @@ static void *host_worker(void *arg)
   pthread_mutex_lock(&b->mu);
   for (;;)
   {
-    while (!b->q_n)
+    while (!b->q_n && !b->stop)
       pthread_cond_wait(&b->cv, &b->mu);
+    if (!b->q_n)
+      break;   /* stopped, nothing queued */
     const int k = b->q[b->q_head];
     pthread_mutex_unlock(&b->mu);
     host_parse(b, k);
@@ -127,6 +147,7 @@ static void *host_worker(void *arg)
     (void) r;
     pthread_mutex_lock(&b->mu);
   }
+  pthread_mutex_unlock(&b->mu);
   return NULL;
 }
 
@@ -140,8 +161,10 @@ static void *gpu_waiter(void *arg)
   pthread_mutex_lock(&b->mu);
   for (;;)
   {
-    while (!b->q_n)
+    while (!b->q_n && !b->stop)
       pthread_cond_wait(&b->cv, &b->mu);
+    if (!b->q_n)
+      break;   /* stopped, nothing queued */
     const int k = b->q[b->q_head];
     pthread_mutex_unlock(&b->mu);
     if (b->complete == COMPLETE_SPIN)
@@ -161,6 +184,7 @@ static void *gpu_waiter(void *arg)
     (void) r;
     pthread_mutex_lock(&b->mu);
   }
+  pthread_mutex_unlock(&b->mu);
   return NULL;
 }
 
@@ -173,10 +197,11 @@ static uint64_t now_ns(void)
 
 static void print_stats(void)
 {
+  const uint64_t r = __atomic_load_n(&st_rounds, __ATOMIC_RELAXED), q = __atomic_load_n(&st_requests, __ATOMIC_RELAXED);
+  const uint64_t ns = __atomic_load_n(&st_ns, __ATOMIC_RELAXED);
   fprintf(stderr, "reactor parser %s: %llu rounds, %llu requests (%.1f per round), %.1f us per round (submit to result)\n",
-          B.parser == PARSER_GPU ? "gpu" : "host", (unsigned long long) B.st_rounds, (unsigned long long) B.st_requests,
-          B.st_rounds ? (double) B.st_requests / (double) B.st_rounds : 0.0,
-          B.st_rounds ? (double) B.st_ns / 1e3 / (double) B.st_rounds : 0.0);
+          getenv("RHP_REACTOR_PARSER") ? getenv("RHP_REACTOR_PARSER") : "gpu", (unsigned long long) r,
+          (unsigned long long) q, r ? (double) q / (double) r : 0.0, r ? (double) ns / 1e3 / (double) r : 0.0);
 }
 
 static void die(const char *what, int e)
@@ -188,51 +213,65 @@ static void die(const char *what, int e)
 
 #define HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) die(#x, (int) e_); } while (0)
 
+static void stats_init(void)
+{
+  const char *st = getenv("RHP_REACTOR_STATS");
+  if ((st_on = st && *st == '1'))
+    atexit(print_stats);
+}
+
 static int parser(void)
 {
-  if (B.parser == PARSER_UNSET)
+  if (!B)
+  {
+    static pthread_once_t stats_once = PTHREAD_ONCE_INIT;
+    pthread_once(&stats_once, stats_init);
+    pthread_once(&batch_once, batch_key_init);
+    if (!(B = calloc(1, sizeof *B)))
+      abort();
+    if (pthread_setspecific(batch_key, B) != 0)
+      abort();
+  }
+  if (B->parser == PARSER_UNSET)
   {
     const char *e = getenv("RHP_REACTOR_PARSER");
-    B.parser = !e ? PARSER_GPU : strcmp(e, "host") == 0 ? PARSER_HOST : strcmp(e, "host-async") == 0 ? PARSER_HOST_ASYNC
+    B->parser = !e ? PARSER_GPU : strcmp(e, "host") == 0 ? PARSER_HOST : strcmp(e, "host-async") == 0 ? PARSER_HOST_ASYNC
                                                                                                        : PARSER_GPU;
-    const char *st = getenv("RHP_REACTOR_STATS");
-    if ((B.stats = st && *st == '1'))
-      atexit(print_stats);
     const char *dg = getenv("RHP_REACTOR_DIAG");
-    B.diag_host = dg && strcmp(dg, "hostparse") == 0;
-    B.efd = -1;
-    if (B.parser == PARSER_GPU)
+    B->diag_host = dg && strcmp(dg, "hostparse") == 0;
+    B->efd = -1;
+    if (B->parser == PARSER_GPU)
     {
       int n = 0;
       HIP(hipGetDeviceCount(&n));
       if (n < 1)
         die("hipGetDeviceCount", 0);
-      HIP(hipStreamCreateWithFlags(&B.stream, hipStreamNonBlocking));
+      HIP(hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking));
       const char *c = getenv("RHP_REACTOR_COMPLETE");
-      B.complete = !c ? COMPLETE_EVENT : strcmp(c, "hostfunc") == 0 ? COMPLETE_HOSTFUNC
+      B->complete = !c ? COMPLETE_EVENT : strcmp(c, "hostfunc") == 0 ? COMPLETE_HOSTFUNC
                                        : strcmp(c, "spin") == 0   ? COMPLETE_SPIN
                                                                   : COMPLETE_EVENT;
-      if (B.complete != COMPLETE_HOSTFUNC)
+      if (B->complete != COMPLETE_HOSTFUNC)
         for (int k = 0; k < REACTOR_BATCH_SLOTS; k++)
-          HIP(hipEventCreateWithFlags(&B.ev[k], hipEventDisableTiming |
-                                                    (B.complete == COMPLETE_EVENT ? hipEventBlockingSync : 0)));
+          HIP(hipEventCreateWithFlags(&B->ev[k], hipEventDisableTiming |
+                                                    (B->complete == COMPLETE_EVENT ? hipEventBlockingSync : 0)));
     }
-    if (B.parser != PARSER_HOST)
+    if (B->parser != PARSER_HOST)
     {
-      B.efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
-      if (B.efd < 0)
+      B->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+      if (B->efd < 0)
         die("eventfd", errno);
     }
-    if (B.parser == PARSER_HOST_ASYNC || (B.parser == PARSER_GPU && B.complete != COMPLETE_HOSTFUNC))
+    if (B->parser == PARSER_HOST_ASYNC || (B->parser == PARSER_GPU && B->complete != COMPLETE_HOSTFUNC))
     {
-      pthread_mutex_init(&B.mu, NULL);
-      pthread_cond_init(&B.cv, NULL);
-      if (pthread_create(&B.worker, NULL, B.parser == PARSER_GPU ? gpu_waiter : host_worker, &B) != 0)
+      pthread_mutex_init(&B->mu, NULL);
+      pthread_cond_init(&B->cv, NULL);
+      if (pthread_create(&B->worker, NULL, B->parser == PARSER_GPU ? gpu_waiter : host_worker, B) != 0)
         abort();
-      pthread_detach(B.worker);
+      B->have_worker = 1;
     }
   }
-  return B.parser;
+  return B->parser;
 }
 
 const char *reactor_parser_name(void)
@@ -249,13 +288,13 @@ int reactor_batch_async(void)
 int reactor_batch_fd(void)
 {
   (void) parser();
-  return B.efd;
+  return B->efd;
 }
 
 static void *host_alloc(size_t n)
 {
   void *p = NULL;
-  if (B.parser == PARSER_GPU)
+  if (B->parser == PARSER_GPU)
     HIP(hipHostMalloc(&p, n, hipHostMallocDefault));
   else if (!(p = malloc(n)))
     abort();
@@ -266,7 +305,7 @@ static void host_free(void *p)
 {
   if (!p)
     return;
-  if (B.parser == PARSER_GPU)
+  if (B->parser == PARSER_GPU)
     (void) hipHostFree(p);
   else
     free(p);
@@ -284,7 +323,7 @@ static size_t up16(size_t x) { return (x + 15u) & ~(size_t) 15u; }
 uint8_t *reactor_batch_reserve(int k, size_t bytes, uint32_t n, uint32_t n_sessions)
 {
   (void) parser();
-  slot_t *s = &B.slot[k];
+  slot_t *s = &B->slot[k];
   s->o_off = up16(bytes + RHP_PAD);
   s->o_sess = s->o_off + up16((n + 1u) * sizeof(uint64_t));
   s->in_size = s->o_sess + up16(n_sessions * sizeof(rhp_session_t));
@@ -303,14 +342,14 @@ uint8_t *reactor_batch_reserve(int k, size_t bytes, uint32_t n, uint32_t n_sessi
       c *= 2;
     host_free(s->h_buf);
     s->h_buf = host_alloc(c);
-    if (B.parser == PARSER_GPU)
+    if (B->parser == PARSER_GPU)
     {
       dev_free((void **) &s->d_buf);
       HIP(hipMalloc((void **) &s->d_buf, c));
-      if (!B.d_work)
+      if (!B->d_work)
       {
-        HIP(hipMalloc(&B.d_work, RHP_WORK_WORDS * sizeof(uint32_t)));
-        HIP(hipMemsetAsync(B.d_work, 0, RHP_WORK_WORDS * sizeof(uint32_t), B.stream));
+        HIP(hipMalloc(&B->d_work, RHP_WORK_WORDS * sizeof(uint32_t)));
+        HIP(hipMemsetAsync(B->d_work, 0, RHP_WORK_WORDS * sizeof(uint32_t), B->stream));
       }
     }
     s->cap = c;
@@ -328,12 +367,12 @@ uint8_t *reactor_batch_reserve(int k, size_t bytes, uint32_t n, uint32_t n_sessi
 
 uint64_t *reactor_batch_offsets(int k)
 {
-  return B.slot[k].h_off;
+  return B->slot[k].h_off;
 }
 
 rhp_session_t *reactor_batch_sessions(int k)
 {
-  return B.slot[k].h_sess;
+  return B->slot[k].h_sess;
 }
 
 /* runs on a HIP runtime thread once the round's copies have landed: wake the
@@ -358,32 +397,32 @@ static void host_parse(batch_state_t *st, int k)
 
 void reactor_batch_submit(int k, uint32_t n, size_t bytes, uint32_t n_sessions)
 {
-  slot_t *s = &B.slot[k];
+  slot_t *s = &B->slot[k];
   s->n = n;
   s->n_sess = n_sessions;
   s->bytes = bytes;
-  s->t_submit = B.stats ? now_ns() : 0;
+  s->t_submit = st_on ? now_ns() : 0;
   memset(s->h_bytes + bytes, 0, RHP_PAD);
   s->h_off[n] = bytes;
-  if (B.parser == PARSER_HOST_ASYNC)
+  if (B->parser == PARSER_HOST_ASYNC)
   {
-    pthread_mutex_lock(&B.mu);
-    if (B.q_n >= REACTOR_BATCH_SLOTS)
-      die("reactor_batch_submit: queue full", B.q_n);
-    B.q[(B.q_head + B.q_n) % REACTOR_BATCH_SLOTS] = k;
-    B.q_n++;
-    pthread_cond_broadcast(&B.cv);
-    pthread_mutex_unlock(&B.mu);
+    pthread_mutex_lock(&B->mu);
+    if (B->q_n >= REACTOR_BATCH_SLOTS)
+      die("reactor_batch_submit: queue full", B->q_n);
+    B->q[(B->q_head + B->q_n) % REACTOR_BATCH_SLOTS] = k;
+    B->q_n++;
+    pthread_cond_broadcast(&B->cv);
+    pthread_mutex_unlock(&B->mu);
     return;
   }
-  if (B.parser == PARSER_HOST || B.diag_host)
+  if (B->parser == PARSER_HOST || B->diag_host)
   {
-    host_parse(&B, k);
-    if (B.parser == PARSER_GPU)
-      round_done((void *) (intptr_t) B.efd);   /* diagnostic mode keeps the asynchronous protocol */
+    host_parse(B, k);
+    if (B->parser == PARSER_GPU)
+      round_done((void *) (intptr_t) B->efd);   /* diagnostic mode keeps the asynchronous protocol */
     return;
   }
-  HIP(hipMemcpyAsync(s->d_buf, s->h_buf, s->in_size, hipMemcpyHostToDevice, B.stream));   /* bytes, offsets, sessions */
+  HIP(hipMemcpyAsync(s->d_buf, s->h_buf, s->in_size, hipMemcpyHostToDevice, B->stream));   /* bytes, offsets, sessions */
   /* the pieces speculatively, then every session walked in order from its
    * true request boundaries (include/rhp.h rhp_fixup_sessions): all of a
    * round's pipelined requests, bodies included, in this one round */
@@ -391,62 +430,84 @@ void reactor_batch_submit(int k, uint32_t n, size_t bytes, uint32_t n_sessions)
   rhp_batch_t b = {
     .bytes = d, .bytes_rw = d, .offsets = (const uint64_t *) (d + s->o_off), .bytes_size = bytes + RHP_PAD, .n = n,
     .max_headers = REACTOR_BATCH_HEADERS, .mode = RHP_MODE_HTTP, .reqs = (rhp_req_t *) (d + s->o_req),
-    .hdrs = (rhp_hdr_t *) (d + s->o_hdr), .http = (rhp_http_t *) (d + s->o_http), .work = B.d_work,
+    .hdrs = (rhp_hdr_t *) (d + s->o_hdr), .http = (rhp_http_t *) (d + s->o_http), .work = B->d_work,
     .flags = RHP_BATCH_SPECULATIVE};
-  int rc = rhp_parse_batch(&b, B.stream);
+  int rc = rhp_parse_batch(&b, B->stream);
   if (rc != 0)
     die("rhp_parse_batch", rc);
   rc = rhp_fixup_sessions(&b, (const rhp_session_t *) (d + s->o_sess), n_sessions,
-                          (rhp_session_result_t *) (d + s->o_sres), (uint64_t *) (d + s->o_start), B.stream);
+                          (rhp_session_result_t *) (d + s->o_sres), (uint64_t *) (d + s->o_start), B->stream);
   if (rc != 0)
     die("rhp_fixup_sessions", rc);
-  /* the records, and the bytes (chunked bodies are de-framed in place by the
-   * fix-up, http.c:155): one asynchronous copy of the whole layout */
-  HIP(hipMemcpyAsync(s->h_buf, s->d_buf, s->out_size, hipMemcpyDeviceToHost, B.stream));
-  if (B.complete == COMPLETE_HOSTFUNC)
+  /* the records: one asynchronous copy of the layout's output part (the
+   * bytes, de-framed in place where a body is chunked, http.c:155, come back
+   * only for a round that has such a body: reactor_batch_result) */
+  HIP(hipMemcpyAsync(s->h_buf + s->o_req, s->d_buf + s->o_req, s->out_size - s->o_req, hipMemcpyDeviceToHost, B->stream));
+  if (B->complete == COMPLETE_HOSTFUNC)
   {
-    HIP(hipLaunchHostFunc(B.stream, round_done, (void *) (intptr_t) B.efd));
+    HIP(hipLaunchHostFunc(B->stream, round_done, (void *) (intptr_t) B->efd));
     return;
   }
-  HIP(hipEventRecord(B.ev[k], B.stream));
-  pthread_mutex_lock(&B.mu);
-  if (B.q_n >= REACTOR_BATCH_SLOTS)
-    die("reactor_batch_submit: queue full", B.q_n);
-  B.q[(B.q_head + B.q_n) % REACTOR_BATCH_SLOTS] = k;
-  B.q_n++;
-  pthread_cond_broadcast(&B.cv);
-  pthread_mutex_unlock(&B.mu);
+  HIP(hipEventRecord(B->ev[k], B->stream));
+  pthread_mutex_lock(&B->mu);
+  if (B->q_n >= REACTOR_BATCH_SLOTS)
+    die("reactor_batch_submit: queue full", B->q_n);
+  B->q[(B->q_head + B->q_n) % REACTOR_BATCH_SLOTS] = k;
+  B->q_n++;
+  pthread_cond_broadcast(&B->cv);
+  pthread_mutex_unlock(&B->mu);
 }
 
 int reactor_batch_completed(void)
 {
   uint64_t v = 0;
-  if (read(B.efd, &v, sizeof v) != (ssize_t) sizeof v)
+  if (read(B->efd, &v, sizeof v) != (ssize_t) sizeof v)
     return 0;
   return (int) v;
 }
 
 void reactor_batch_wait(void)
 {
-  if (B.parser == PARSER_GPU)
-    HIP(hipStreamSynchronize(B.stream));
-  if (B.parser == PARSER_HOST_ASYNC || (B.parser == PARSER_GPU && B.complete != COMPLETE_HOSTFUNC))
+  if (!B)
+    return;
+  if (B->parser == PARSER_GPU)
+    HIP(hipStreamSynchronize(B->stream));
+  if (B->parser == PARSER_HOST_ASYNC || (B->parser == PARSER_GPU && B->complete != COMPLETE_HOSTFUNC))
   {
-    pthread_mutex_lock(&B.mu);
-    while (B.q_n)
-      pthread_cond_wait(&B.cv, &B.mu);
-    pthread_mutex_unlock(&B.mu);
+    pthread_mutex_lock(&B->mu);
+    while (B->q_n)
+      pthread_cond_wait(&B->cv, &B->mu);
+    pthread_mutex_unlock(&B->mu);
   }
 }
 
 void reactor_batch_result(int k, reactor_batch_result_t *out)
 {
-  slot_t *s = &B.slot[k];
-  if (B.stats)
+  slot_t *s = &B->slot[k];
+  if (st_on)
   {
-    B.st_rounds++;
-    B.st_requests += s->n;
-    B.st_ns += now_ns() - s->t_submit;
+    __atomic_fetch_add(&st_rounds, 1, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&st_requests, s->n, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&st_ns, now_ns() - s->t_submit, __ATOMIC_RELAXED);
+  }
+  if (B->parser == PARSER_GPU && !B->diag_host)
+  {
+    /* only the records came back (reactor_batch_submit): the bytes, de-framed
+     * in place by the fix-up, are fetched when some request of the round has a
+     * chunked body (the server copies that body from them, server.c) */
+    bool chunked = false;
+    for (uint32_t i = 0; i < s->n && !chunked; i++)
+    {
+      const rhp_http_t *x = &s->h_http[i];
+      chunked = x->result == 1 && x->body_kind && x->consumed != (uint64_t) s->h_req[i].ret + x->body_len;
+    }
+    if (chunked)
+    {
+      if (!B->cstream)
+        HIP(hipStreamCreateWithFlags(&B->cstream, hipStreamNonBlocking));
+      HIP(hipMemcpyAsync(s->h_buf, s->d_buf, s->bytes, hipMemcpyDeviceToHost, B->cstream));
+      HIP(hipStreamSynchronize(B->cstream));
+    }
   }
   out->bytes = s->h_bytes;
   out->reqs = s->h_req;
@@ -465,21 +526,21 @@ enum { WRITER_HOST, WRITER_HOST_BATCH, WRITER_GPU };
 int reactor_batch_writer(void)
 {
   (void) parser();
-  if (B.writer == 0)
+  if (B->writer == 0)
   {
     const char *e = getenv("RHP_REACTOR_WRITER");
-    B.writer = 1 + (!e ? WRITER_HOST : strcmp(e, "gpu") == 0 ? WRITER_GPU : strcmp(e, "host-batch") == 0 ? WRITER_HOST_BATCH
+    B->writer = 1 + (!e ? WRITER_HOST : strcmp(e, "gpu") == 0 ? WRITER_GPU : strcmp(e, "host-batch") == 0 ? WRITER_HOST_BATCH
                                                                                                         : WRITER_HOST);
-    if (B.writer == 1 + WRITER_GPU && B.parser != PARSER_GPU)
+    if (B->writer == 1 + WRITER_GPU && B->parser != PARSER_GPU)
     {
       /* the gpu writer runs on the gpu parser's device */
       fprintf(stderr, "reactor: RHP_REACTOR_WRITER=gpu needs RHP_REACTOR_PARSER=gpu\n");
       abort();
     }
-    if (B.writer == 1 + WRITER_GPU)
-      HIP(hipStreamCreateWithFlags(&B.wstream, hipStreamNonBlocking));
+    if (B->writer == 1 + WRITER_GPU)
+      HIP(hipStreamCreateWithFlags(&B->wstream, hipStreamNonBlocking));
   }
-  return B.writer - 1 != WRITER_HOST;
+  return B->writer - 1 != WRITER_HOST;
 }
 
 static void grow_dev(void **p, size_t *cap, size_t need)
@@ -499,7 +560,7 @@ void reactor_batch_write(const uint8_t *arena, size_t arena_n, const rhp_resp_t 
                          const rhp_resp_field_t *fields, uint32_t n_fields, const char *date, const uint8_t **out,
                          const uint64_t **out_off)
 {
-  if (B.writer - 1 == WRITER_HOST_BATCH)
+  if (B->writer - 1 == WRITER_HOST_BATCH)
   {
     /* the host serializer, into one buffer in reply order */
     static __thread buffer_t buf;
@@ -537,51 +598,132 @@ void reactor_batch_write(const uint8_t *arena, size_t arena_n, const rhp_resp_t 
   }
   /* gpu: H2D of the round's replies, rhp_write_responses, D2H (synchronous, on
    * the writer's own stream: the next parse round, already queued on
-   * B.wstream, keeps running meanwhile) */
-  grow_dev(&B.dw_arena, &B.w_cap_arena, arena_n + 16);
-  size_t cap_n = B.w_cap_n;
-  grow_dev(&B.dw_resps, &B.w_cap_n, (size_t) n * sizeof *resps + 16);
-  if (B.w_cap_n != cap_n || !B.hw_off)
+   * B->wstream, keeps running meanwhile) */
+  grow_dev(&B->dw_arena, &B->w_cap_arena, arena_n + 16);
+  size_t cap_n = B->w_cap_n;
+  grow_dev(&B->dw_resps, &B->w_cap_n, (size_t) n * sizeof *resps + 16);
+  if (B->w_cap_n != cap_n || !B->hw_off)
   {
-    dev_free(&B.dw_off);
-    dev_free(&B.dw_work);
-    if (B.hw_off)
-      (void) hipHostFree(B.hw_off);
-    const size_t rn = B.w_cap_n / sizeof *resps + 1;
-    HIP(hipMalloc(&B.dw_off, rn * sizeof(uint64_t)));
-    HIP(hipMalloc(&B.dw_work, RHP_RESP_WORK_WORDS(rn) * sizeof(uint64_t)));
-    HIP(hipHostMalloc((void **) &B.hw_off, rn * sizeof(uint64_t), hipHostMallocDefault));
+    dev_free(&B->dw_off);
+    dev_free(&B->dw_work);
+    if (B->hw_off)
+      (void) hipHostFree(B->hw_off);
+    const size_t rn = B->w_cap_n / sizeof *resps + 1;
+    HIP(hipMalloc(&B->dw_off, rn * sizeof(uint64_t)));
+    HIP(hipMalloc(&B->dw_work, RHP_RESP_WORK_WORDS(rn) * sizeof(uint64_t)));
+    HIP(hipHostMalloc((void **) &B->hw_off, rn * sizeof(uint64_t), hipHostMallocDefault));
   }
-  grow_dev(&B.dw_fields, &B.w_cap_f, (size_t) n_fields * sizeof *fields + 16);
-  HIP(hipMemcpyAsync(B.dw_arena, arena, arena_n, hipMemcpyHostToDevice, B.wstream));
-  HIP(hipMemcpyAsync(B.dw_resps, resps, (size_t) n * sizeof *resps, hipMemcpyHostToDevice, B.wstream));
+  grow_dev(&B->dw_fields, &B->w_cap_f, (size_t) n_fields * sizeof *fields + 16);
+  HIP(hipMemcpyAsync(B->dw_arena, arena, arena_n, hipMemcpyHostToDevice, B->wstream));
+  HIP(hipMemcpyAsync(B->dw_resps, resps, (size_t) n * sizeof *resps, hipMemcpyHostToDevice, B->wstream));
   if (n_fields)
-    HIP(hipMemcpyAsync(B.dw_fields, fields, (size_t) n_fields * sizeof *fields, hipMemcpyHostToDevice, B.wstream));
+    HIP(hipMemcpyAsync(B->dw_fields, fields, (size_t) n_fields * sizeof *fields, hipMemcpyHostToDevice, B->wstream));
   for (int pass = 0; pass < 2; pass++)
   {
-    rhp_resp_batch_t w = {.arena = B.dw_arena, .resps = B.dw_resps, .fields = n_fields ? B.dw_fields : NULL, .n = n,
-                          .date_len = RHP_DATE_LEN, .date = date, .out_off = B.dw_off, .out = B.dw_out,
-                          .out_size = B.w_cap_out, .work = B.dw_work};
-    int rc = rhp_write_responses(&w, B.wstream);
+    rhp_resp_batch_t w = {.arena = B->dw_arena, .resps = B->dw_resps, .fields = n_fields ? B->dw_fields : NULL, .n = n,
+                          .date_len = RHP_DATE_LEN, .date = date, .out_off = B->dw_off, .out = B->dw_out,
+                          .out_size = B->w_cap_out, .work = B->dw_work};
+    int rc = rhp_write_responses(&w, B->wstream);
     if (rc != 0)
       die("rhp_write_responses", rc);
-    HIP(hipMemcpyAsync(B.hw_off, B.dw_off, ((size_t) n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, B.wstream));
-    HIP(hipStreamSynchronize(B.wstream));
-    if (B.hw_off[n] <= B.w_cap_out)
+    HIP(hipMemcpyAsync(B->hw_off, B->dw_off, ((size_t) n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, B->wstream));
+    HIP(hipStreamSynchronize(B->wstream));
+    if (B->hw_off[n] <= B->w_cap_out)
       break;
     /* the output did not fit: grow it and write again (rhp.h) */
-    size_t c = B.w_cap_out ? B.w_cap_out : 1u << 20;
-    while (c < B.hw_off[n])
+    size_t c = B->w_cap_out ? B->w_cap_out : 1u << 20;
+    while (c < B->hw_off[n])
       c *= 2;
-    dev_free(&B.dw_out);
-    HIP(hipMalloc(&B.dw_out, c));
-    if (B.hw_out)
-      (void) hipHostFree(B.hw_out);
-    HIP(hipHostMalloc((void **) &B.hw_out, c, hipHostMallocDefault));
-    B.w_cap_out = c;
+    dev_free(&B->dw_out);
+    HIP(hipMalloc(&B->dw_out, c));
+    if (B->hw_out)
+      (void) hipHostFree(B->hw_out);
+    HIP(hipHostMalloc((void **) &B->hw_out, c, hipHostMallocDefault));
+    B->w_cap_out = c;
   }
-  HIP(hipMemcpyAsync(B.hw_out, B.dw_out, B.hw_off[n], hipMemcpyDeviceToHost, B.wstream));
-  HIP(hipStreamSynchronize(B.wstream));
-  *out = B.hw_out;
-  *out_off = B.hw_off;
+  HIP(hipMemcpyAsync(B->hw_out, B->dw_out, B->hw_off[n], hipMemcpyDeviceToHost, B->wstream));
+  HIP(hipStreamSynchronize(B->wstream));
+  *out = B->hw_out;
+  *out_off = B->hw_off;
+}
+
+/* thread exit (pthread key destructor): the rounds in flight complete, the
+ * waiter / worker thread is stopped and joined, then every resource goes */
+static void batch_teardown(void *arg)
+{
+  batch_state_t *b = arg;
+  B = b;   /* the thread's TLS pointer may already be cleared */
+  if (b->parser == PARSER_GPU)
+    (void) hipStreamSynchronize(b->stream);
+  if (b->have_worker)
+  {
+    pthread_mutex_lock(&b->mu);
+    b->stop = 1;
+    pthread_cond_broadcast(&b->cv);
+    pthread_mutex_unlock(&b->mu);
+    (void) pthread_join(b->worker, NULL);
+    pthread_mutex_destroy(&b->mu);
+    pthread_cond_destroy(&b->cv);
+  }
+  for (int k = 0; k < REACTOR_BATCH_SLOTS; k++)
+  {
+    host_free(b->slot[k].h_buf);
+    if (b->parser == PARSER_GPU)
+      dev_free((void **) &b->slot[k].d_buf);
+  }
+  if (b->parser == PARSER_GPU)
+  {
+    if (b->complete != COMPLETE_HOSTFUNC)
+      for (int k = 0; k < REACTOR_BATCH_SLOTS; k++)
+        (void) hipEventDestroy(b->ev[k]);
+    if (b->writer == 1 + WRITER_GPU)
+    {
+      (void) hipStreamSynchronize(b->wstream);
+      dev_free(&b->dw_arena);
+      dev_free(&b->dw_resps);
+      dev_free(&b->dw_fields);
+      dev_free(&b->dw_out);
+      dev_free(&b->dw_off);
+      dev_free(&b->dw_work);
+      if (b->hw_out)
+        (void) hipHostFree(b->hw_out);
+      if (b->hw_off)
+        (void) hipHostFree(b->hw_off);
+      (void) hipStreamDestroy(b->wstream);
+    }
+    dev_free(&b->d_work);
+    if (b->cstream)
+      (void) hipStreamDestroy(b->cstream);
+    (void) hipStreamDestroy(b->stream);
+  }
+  if (b->efd >= 0)
+    close(b->efd);
+  free(b);
+  B = NULL;
+}
+
+void reactor_batch_prepare(void)
+{
+  if (parser() != PARSER_GPU || B->diag_host || B->slot[0].cap || B->slot[1].cap)
+    return;   /* host parsers need no warm-up; slots in use: the thread's rounds have begun */
+  /* Everything a first round would otherwise pay inside a client's burst: the
+   * pinned and device slots at their first capacity, the code object's load,
+   * the kernels' first launches and the completion path, by one round of one
+   * request through the whole protocol, waited for here. */
+  static const char warm[] = "GET / HTTP/1.1\r\nHost: warm-up\r\n\r\n";
+  const size_t n = sizeof warm - 1;
+  for (int k = REACTOR_BATCH_SLOTS - 1; k >= 0; k--)
+  {
+    uint8_t *h = reactor_batch_reserve(k, n, 1, 1);
+    memcpy(h, warm, n);
+    reactor_batch_offsets(k)[0] = 0;
+    rhp_session_t *ss = reactor_batch_sessions(k);
+    ss[0].piece_lo = 0;
+    ss[0].piece_hi = 1;
+    reactor_batch_submit(k, 1, n, 1);
+  }
+  reactor_batch_wait();
+  uint64_t v;
+  while (read(B->efd, &v, sizeof v) == (ssize_t) sizeof v)
+    ;   /* the warm-up rounds' completions are nobody's */
 }

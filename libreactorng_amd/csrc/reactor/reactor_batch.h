@@ -29,6 +29,10 @@ typedef struct reactor_batch_result
 /* 1: rounds complete asynchronously (gpu parser) and each completion adds 1 to
  * the eventfd reactor_batch_fd(); 0: reactor_batch_submit parses in place */
 int       reactor_batch_async(void);
+/* once per thread, before its first round (server_open): the gpu parser's
+ * slots, code object and first launches set up by one warm-up round, so no
+ * client's first burst pays for them */
+void      reactor_batch_prepare(void);
 int       reactor_batch_fd(void);
 /* staging of slot k for `bytes` packed input bytes (+ RHP_PAD), n pieces and
  * n_sessions sessions */

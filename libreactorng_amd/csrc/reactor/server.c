@@ -197,7 +197,22 @@ static __thread struct
   reactor_t  poll;       /* the batch eventfd, registered while count > 0 */
   server_t **waiting;    /* servers turned away while every slot was in flight */
   size_t     n_waiting, cap_waiting;
+  int        servers;    /* constructed and not yet destructed on this thread */
 } R;
+
+/* the last server of the thread is gone: the rounds' arrays go too */
+static void rounds_release(void)
+{
+  for (int k = 0; k < REACTOR_BATCH_SLOTS; k++)
+  {
+    free(R.r[k].sessions);
+    free(R.r[k].pieces);
+    R.r[k] = (round_t) {0};
+  }
+  free(R.waiting);
+  R.waiting = NULL;
+  R.n_waiting = R.cap_waiting = 0;
+}
 
 
 static void *grow(void *p, size_t *cap, size_t need, size_t elem)
@@ -333,7 +348,6 @@ static bool server_session_dispatch(server_session_t *s, uint32_t lo, const rhp_
       result = http_read_request(&s->stream, &s->request.method, &s->request.target, &s->request.body,
                                  s->request.fields, &s->request.fields_count);
       consumed = before - data_size(stream_read(&s->stream));
-      more = true;
     }
     if (result == -1)
     {
@@ -341,7 +355,9 @@ static bool server_session_dispatch(server_session_t *s, uint32_t lo, const rhp_
       return true;
     }
     if (result == 0)
-      break;
+      break;   /* incomplete (a TOOLONG request too): the session waits for more bytes */
+    if (x->result == RHP_RET_TOOLONG)
+      more = true;   /* parsed on the host: the rest of the input goes to the next batch */
     if (x->result != RHP_RET_TOOLONG)
     {
       uint8_t *base = data_base(in);
@@ -375,6 +391,9 @@ static bool server_session_dispatch(server_session_t *s, uint32_t lo, const rhp_
 /* RHP_REACTOR_STATS=1: time per round phase (split+pack+submit, dispatch), at exit */
 static int round_stats = -1;
 static uint64_t rs_pack_ns, rs_dispatch_ns, rs_rounds;
+static uint64_t rounds_total;   /* rounds submitted with input, every server of the process */
+
+uint64_t reactor_batch_rounds(void) { return __atomic_load_n(&rounds_total, __ATOMIC_RELAXED); }
 static uint64_t rs_now(void)
 {
   struct timespec ts;
@@ -555,6 +574,7 @@ static void server_batch_run(reactor_event_t *event)
       at += data_size(in);
     }
     reactor_batch_submit(k, (uint32_t) r->n_pieces, bytes, (uint32_t) r->n_sessions);
+    __atomic_fetch_add(&rounds_total, 1, __ATOMIC_RELAXED);
   }
   if (round_stats)
   {
@@ -599,6 +619,7 @@ static void server_rounds_drain(server_t *server)
 void server_construct(server_t *server, reactor_callback_t *callback, void *state)
 {
   *server = (server_t) {.user = reactor_user_define(callback, state)};
+  R.servers++;
   list_init(&server->sessions);
   list_init(&server->queue);
   timeout_construct(&server->timeout, server_timeout, NULL);
@@ -622,11 +643,17 @@ void server_destruct(server_t *server)
   if (server->batch)
     reactor_cancel(server->batch, NULL, NULL);
   server->batch = 0;
+  if (--R.servers <= 0 && !R.count)
+  {
+    R.servers = 0;
+    rounds_release();
+  }
 }
 
 void server_open(server_t *server, const char *host, int port)
 {
   server->accept = network_accept(server_accept, server, host, port, NETWORK_REUSEADDR);
+  reactor_batch_prepare();   /* the parser's setup before any client's first burst */
   timeout_set(&server->timeout, (reactor_now() / 1000000000) * 1000000000, 1000000000);
   server_date_update();
 }
@@ -634,6 +661,7 @@ void server_open(server_t *server, const char *host, int port)
 void server_open_socket(server_t *server, int socket)
 {
   server->accept = network_accept_socket(server_accept, server, socket);
+  reactor_batch_prepare();   /* the parser's setup before any client's first burst */
   timeout_set(&server->timeout, (reactor_now() / 1000000000) * 1000000000, 1000000000);
   server_date_update();
 }

@@ -69,6 +69,8 @@ struct Params {
 #endif
 
 enum : uint32_t {
+  kSecDecodeStamp = 6,                           /* Diag section slots of the late form's decode / framing */
+  kSecFrameStamp = 7,
   kBlock = 128,                                  /* window bytes per lane per loop iteration */
   kParts = kBlock / 16,                          /* 16-byte parts per window */
   kEvWords = kBlock / 32,                        /* 32-bit event words per window */
@@ -123,29 +125,127 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
+/* s_waitcnt vmcnt(0) / lgkmcnt(0), as inline asm (invisible to the compiler's
+ * wait insertion, which would otherwise add waits of its own around them) */
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+/* Diagnostics.  The kernel calls the methods of one `Diag` object at its
+ * section boundaries; in product builds every method is empty and the object
+ * has no state, so the hot loop compiles as if the calls were not there.
+ *
+ * RHP_STAMPS (diagnostic build, tools/stamps2.py): per-wave shader-cycle sums
+ * per loop section and realtime (100 MHz) marks, stored by each wave's lane 0
+ * into a buffer of its own (never read by the kernel): slots 0-4 section
+ * cycles, 5 iterations, 6 entry, 7 loop start, 8 loop end, 9 exit, 10
+ * lane-windows walked, 11 lane-iterations without a window to walk, 12 of them
+ * while the pool still had requests, 13 iterations after the pool ran dry, 14
+ * the replay's start (after the workgroup barrier), 15 / 16 the wave's shader
+ * cycles in the replay's pass 2 (listed scalar paths) / pass 1, 17 requests it
+ * ran in pass 2, 18 requests it framed in pass 1, 19 the prologue's loads
+ * landed, 20 / 21 late form: decode_window / frame_window cycles (inside
+ * section 2).  A section that ends with a wait (`sync`) waits for its LDS reads
+ * (and, where named, its memory) first, so its cycles include their latency.
+ * RHP_CLOCK (diagnostic build, tools/kclock.py): shader ticks and 100 MHz
+ * ticks from the entry of block 0 wave 0 to its loop's end. */
 #ifdef RHP_STAMPS
-/* diagnostic build only: per-wave shader-cycle sums per loop section and
- * realtime (100 MHz) marks, stored by each wave's lane 0 into a buffer of its
- * own (never read by the kernel): slots 0-4 section cycles, 5 iterations,
- * 6 entry, 7 loop start, 8 loop end, 9 exit, 10 lane-windows walked,
- * 11 lane-iterations without a window to walk, 12 of them while the pool
- * still had requests, 13 iterations after the pool ran dry, 14 the replay's
- * start (after the workgroup barrier), 15 / 16 the wave's shader cycles in the
- * replay's pass 2 (listed scalar paths) / pass 1, 17 requests it ran in pass 2,
- * 18 requests it framed in pass 1, 19 the prologue's loads landed */
 enum : uint32_t { kStampSlots = 24 };
 __device__ unsigned long long g_stamps[8192 * kStampSlots];
-#define RHP_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); (t) = __builtin_amdgcn_s_memtime(); \
-    __builtin_amdgcn_sched_barrier(0); } while (0)
-#else
-#define RHP_STAMP(t) do { } while (0)
 #endif
 #ifdef RHP_CLOCK
-/* diagnostic build only: shader ticks and 100 MHz real-time ticks from the
- * entry of the first wave to its exit, written by block 0 wave 0 (never read
- * by the kernel); the quotient is the shader clock the kernel ran at */
 __device__ unsigned long long g_clock[2];
 #endif
+struct Diag {
+#ifdef RHP_STAMPS
+  unsigned long long t0 = 0, t1 = 0, c0 = 0, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rp[4] = {0, 0, 0, 0};
+  unsigned long long rt_entry = 0, rt_loads = 0, rt_loop = 0, n_walk = 0, n_idle = 0, n_idle_live = 0, n_dry = 0;
+  __device__ static unsigned long long now()
+  {
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+  }
+  __device__ unsigned long long *slots(uint32_t waves) const
+  {
+    return g_stamps + ((blockIdx.x * waves + (threadIdx.x >> 6)) % 8192u) * kStampSlots;
+  }
+  __device__ void entry() { rt_entry = __builtin_amdgcn_s_memrealtime(); }
+  __device__ void loads_landed() { rt_loads = __builtin_amdgcn_s_memrealtime(); }
+  __device__ void loop_start() { rt_loop = __builtin_amdgcn_s_memrealtime(); }
+  __device__ void mark() { t0 = now(); }
+  /* the section that began at the last mark ends here: its cycles into acc[k] */
+  __device__ void section(uint32_t k, bool lgkm = false, bool vm = false)
+  {
+    if (vm) wait_vm0();
+    if (lgkm) wait_lgkm0();
+    t1 = now();
+    acc[k] += t1 - t0;
+    t0 = t1;
+  }
+  __device__ void lanes(bool walking, bool pool_dry)
+  {
+    n_walk += __popcll(__builtin_amdgcn_ballot_w64(walking));
+    n_idle += __popcll(__builtin_amdgcn_ballot_w64(!walking));
+    if (!pool_dry) n_idle_live += __popcll(__builtin_amdgcn_ballot_w64(!walking));
+    else n_dry++;
+  }
+  __device__ void iteration_end() { section(4); acc[5] += 1; }
+  __device__ void loop_end(uint32_t waves)
+  {
+    if ((threadIdx.x & 63u) != 0) return;
+    unsigned long long *g = slots(waves);
+    for (int k = 0; k < 6; k++) g[k] = acc[k];
+    g[6] = rt_entry; g[7] = rt_loop; g[8] = __builtin_amdgcn_s_memrealtime();
+    g[10] = n_walk; g[11] = n_idle; g[12] = n_idle_live; g[13] = n_dry; g[19] = rt_loads;
+    g[20] = acc[kSecDecodeStamp]; g[21] = acc[kSecFrameStamp];
+  }
+  __device__ void replay_start(uint32_t waves)
+  {
+    if ((threadIdx.x & 63u) == 0) slots(waves)[14] = __builtin_amdgcn_s_memrealtime();
+  }
+  __device__ void pass_begin() { c0 = now(); }
+  __device__ void pass_end(uint32_t k) { rp[k] += now() - c0; }   /* 0: pass 2, 1: pass 1 */
+  __device__ void framed(bool done) { rp[3] += __popcll(__builtin_amdgcn_ballot_w64(done)); }
+  __device__ void slow_path() { rp[2] += __popcll(__builtin_amdgcn_ballot_w64(true)); }
+  __device__ void exit(uint32_t waves)
+  {
+    if ((threadIdx.x & 63u) != 0) return;
+    unsigned long long *g = slots(waves);
+    g[9] = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < 4; k++) g[15 + k] = rp[k];
+  }
+#else
+  __device__ void entry() {}
+  __device__ void loads_landed() {}
+  __device__ void loop_start() {}
+  __device__ void mark() {}
+  __device__ void section(uint32_t, bool = false, bool = false) {}
+  __device__ void lanes(bool, bool) {}
+  __device__ void iteration_end() {}
+  __device__ void loop_end(uint32_t) {}
+  __device__ void replay_start(uint32_t) {}
+  __device__ void pass_begin() {}
+  __device__ void pass_end(uint32_t) {}
+  __device__ void framed(bool) {}
+  __device__ void slow_path() {}
+  __device__ void exit(uint32_t) {}
+#endif
+#ifdef RHP_CLOCK
+  unsigned long long clk_t0 = 0, clk_r0 = 0;
+  __device__ void clock_start() { clk_t0 = __builtin_amdgcn_s_memtime(); clk_r0 = __builtin_amdgcn_s_memrealtime(); }
+  __device__ void clock_end()
+  {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      g_clock[0] = __builtin_amdgcn_s_memtime() - clk_t0;
+      g_clock[1] = __builtin_amdgcn_s_memrealtime() - clk_r0;
+    }
+  }
+#else
+  __device__ void clock_start() {}
+  __device__ void clock_end() {}
+#endif
+};
 
 /* The exact parser's byte reader on the GPU: the aligned 16-byte line holding
  * the last byte read stays in registers, so its sequential scan makes one
@@ -438,11 +538,6 @@ __device__ __forceinline__ void ev_shift2(uint32_t &ev, uint32_t idx)
   asm("v_alignbit_b32 %0, %1, %0, 2" : "+v"(ev) : "v"(idx));
 }
 
-/* s_waitcnt vmcnt(0) / lgkmcnt(0), as inline asm (invisible to the compiler's
- * wait insertion, which would otherwise add waits of its own around them) */
-__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
 /* one byte of LDS at address a (the table is at LDS address 0) */
 __device__ __forceinline__ uint32_t lds_u8(uint32_t a)
 {
@@ -510,12 +605,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
-#ifdef RHP_STAMPS
-  const unsigned long long rt_entry = __builtin_amdgcn_s_memrealtime();
-#endif
-#ifdef RHP_CLOCK
-  const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
+  Diag dg;   /* diagnostic builds only; nothing in product builds */
+  dg.entry();
+  dg.clock_start();
 
   const uint32_t maxh = p.max_headers;
   constexpr bool http = HTTP;   /* p.mode == RHP_MODE_HTTP (the launch picks the instance) */
@@ -1134,9 +1226,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   for (uint32_t k = tid; k < kPoolWords; k += WAVES * 64)
     reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave)[k] = k == 0 ? first_n : 0u;
   wait_vm0();   /* the pending offsets */
-#ifdef RHP_STAMPS
-  const unsigned long long rt_loads = __builtin_amdgcn_s_memrealtime();
-#endif
+  dg.loads_landed();
   const bool uneven =
       may_order && __builtin_amdgcn_ballot_w64((uint64_t) (s1 - s0) * span_n > 2u * (o_hi - o_lo)) != 0;
   /* An uneven range runs on 12 of the 16 waves: its end is set by its longest
@@ -1183,11 +1273,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * previous window -> [F] walk this one -> [G] finalize the
    * decoded request if it ended, hand the decode over to the walked window.
    */
-#ifdef RHP_STAMPS
-  unsigned long long t0 = 0, t1 = 0, acc[6] = {0, 0, 0, 0, 0, 0}, acc_dw = 0, acc_fw = 0;
-  const unsigned long long rt_loop = __builtin_amdgcn_s_memrealtime();
-  unsigned long long n_walk = 0, n_idle = 0, n_idle_live = 0, n_dry = 0;
-#endif
+  dg.loop_start();
   /* The SIMD issues by priority, then age: with equal priorities the waves
    * dispatched last in a workgroup run slowest and finish its range last.
    * Rotating every wave's priority each iteration (phase by wave) shares the
@@ -1204,12 +1290,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     case 2: __builtin_amdgcn_s_setprio(2); break;
     default: __builtin_amdgcn_s_setprio(3);
     }
-    RHP_STAMP(t0);
+    dg.mark();
     /* [A] */
     wait_vm0();   /* the window's LDS-DMA has landed (and the pending offsets, and older stores) */
-#ifdef RHP_STAMPS
-    RHP_STAMP(t1); acc[0] += t1 - t0; t0 = t1;
-#endif
+    dg.section(0);
     const uint32_t p_o0 = pend_o0, p_o1 = pend_o1;
 #pragma unroll
     for (int q = 0; q < (int) kParts; q++) W[q] = *reinterpret_cast<const u32x4 *>(lds + stage + stage_off(lane, q));
@@ -1238,12 +1322,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     refill_pend();
     const bool any_walk = __builtin_amdgcn_ballot_w64(walking) != 0;
     const bool any_dec = __builtin_amdgcn_ballot_w64(dhas) != 0;
-#ifdef RHP_STAMPS
-    n_walk += __popcll(__builtin_amdgcn_ballot_w64(walking));
-    n_idle += __popcll(__builtin_amdgcn_ballot_w64(!walking));
-    if (!pool_dry) n_idle_live += __popcll(__builtin_amdgcn_ballot_w64(!walking));
-    else n_dry++;
-#endif
+    dg.lanes(walking, pool_dry);
     if constexpr (!LATE) {
       /* [E] next window: continuation of wcur, else the first window of a ready pend */
       nw = 0;
@@ -1251,19 +1330,13 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       else if (pend_ready) nw = ((p_o0 & ~3u) - (uint32_t) base) | 2u;
       wait_lgkm0();   /* [A]'s reads of the buffer are done */
       issue();
-#ifdef RHP_STAMPS
-      wait_lgkm0();
-      RHP_STAMP(t1); acc[1] += t1 - t0; t0 = t1;
-#endif
+      dg.section(1, true);
       /* [F] walk + decode of the previous window */
       decode_begin();
       if (any_dec) decode_window();
 #pragma unroll
       for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
-#ifdef RHP_STAMPS
-      wait_vm0(); wait_lgkm0();
-      RHP_STAMP(t1); acc[2] += t1 - t0; t0 = t1;
-#endif
+      dg.section(2, true, true);
       if (any_walk) {
         if (!walking) st = kPark;   /* idle lanes step in the parked terminal state */
         walk();
@@ -1277,19 +1350,14 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
        * ready (its offsets landed meanwhile), so a lane never idles an
        * iteration between two requests */
       (void) any_dec;
-#ifdef RHP_STAMPS
-      RHP_STAMP(t1); acc[1] += t1 - t0; t0 = t1;
-#endif
+      dg.section(1);
 #pragma unroll
       for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
       if (any_walk) {
         if (!walking) st = kPark;
         walk();
       }
-#ifdef RHP_STAMPS
-      wait_lgkm0();
-      RHP_STAMP(t1); acc[3] += t1 - t0; t0 = t1;
-#endif
+      dg.section(3, true);
       if (walking && wnew) {
         dcur = wcur;
         dlen = wlen;
@@ -1308,18 +1376,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       decode_begin();
       const uint32_t crec_before = crec_lo | (cand & 0xbfffffffu);
       if (any_walk) decode_window();
-#ifdef RHP_STAMPS
-      wait_lgkm0(); RHP_STAMP(t1); acc_dw += t1 - t0; t0 = t1;
-#endif
+      dg.section(kSecDecodeStamp, true);
       if (http && any_walk) frame_window(crec_before);
-#ifdef RHP_STAMPS
-      wait_lgkm0(); RHP_STAMP(t1); acc_fw += t1 - t0; t0 = t1;
-#endif
+      dg.section(kSecFrameStamp, true);
       const bool done = any_walk ? decode_end() : false;
-#ifdef RHP_STAMPS
-      wait_lgkm0();
-      RHP_STAMP(t1); acc[2] += t1 - t0; t0 = t1;
-#endif
+      dg.section(2, true);
       /* the walk of wcur ends with this window: finalized (a terminal, a
        * max_headers stop), or its last byte */
       if (walking && (done || is_done2(st) || is_err2(st) || is_slow2(st) ||
@@ -1332,10 +1393,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       wait_lgkm0();
       issue();
     }
-#ifdef RHP_STAMPS
-    wait_lgkm0();
-    RHP_STAMP(t1); acc[LATE ? 4 : 3] += t1 - t0; t0 = t1;
-#endif
+    dg.section(LATE ? 4 : 3, true);
     /* [G] */
     if constexpr (!LATE) {
     const bool done = any_dec ? decode_end() : false;
@@ -1362,34 +1420,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     }
     }
     wpos += (int32_t) kBlock;
-#ifdef RHP_STAMPS
-    RHP_STAMP(t1); acc[4] += t1 - t0; acc[5] += 1;
-#endif
+    dg.iteration_end();
     if (!__ballot(dhas || nw || pend_ok)) break;
   }
-#ifdef RHP_STAMPS
-  if (lane == 0) {
-    const uint32_t w = (blockIdx.x * WAVES + (tid >> 6)) % 8192;
-    for (int k = 0; k < 6; k++) g_stamps[w * kStampSlots + k] = acc[k];
-    g_stamps[w * kStampSlots + 6] = rt_entry;
-    g_stamps[w * kStampSlots + 7] = rt_loop;
-    g_stamps[w * kStampSlots + 8] = __builtin_amdgcn_s_memrealtime();
-    g_stamps[w * kStampSlots + 10] = n_walk;
-    g_stamps[w * kStampSlots + 11] = n_idle;
-    g_stamps[w * kStampSlots + 12] = n_idle_live;
-    g_stamps[w * kStampSlots + 13] = n_dry;
-    g_stamps[w * kStampSlots + 19] = rt_loads;
-    g_stamps[w * kStampSlots + 20] = acc_dw;   /* late form: decode_window cycles (within section 2) */
-    g_stamps[w * kStampSlots + 21] = acc_fw;   /* late form: frame_window cycles (within section 2) */
-  }
-#endif
-#ifdef RHP_CLOCK
-  if (blockIdx.x == 0 && tid == 0) {
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-    g_clock[0] = t1 - clk_t0;
-    g_clock[1] = r1 - clk_r0;
-  }
-#endif
+  dg.loop_end(WAVES);
+  dg.clock_end();
 
   /* Replay: the rare paths run here, after the DFA loop, so none of their
    * registers are live in it.  Once every wave of the workgroup is done, the
@@ -1403,10 +1438,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * side by side.  Nothing to do -> no pass at all. */
   wait_vm0();   /* no window load still writes the staging area (reused below) */
   __syncthreads();
-#ifdef RHP_STAMPS
-  if (lane == 0) g_stamps[((blockIdx.x * WAVES + (tid >> 6)) % 8192) * kStampSlots + 14] = __builtin_amdgcn_s_memrealtime();
-  unsigned long long rp[4] = {0, 0, 0, 0};
-#endif
+  dg.replay_start(WAVES);
   if (*wg_deferred) {
     typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
     /* what a request needs first: in http mode the hint left in its http
@@ -1445,10 +1477,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     uint32_t *slow = reinterpret_cast<uint32_t *>(lds + kLdsTable);   /* the staging area, idle now */
     uint32_t *slow_n = wg_counter + 4;                                 /* 0 since the prologue */
     constexpr uint32_t kSlowCap = WAVES * kStageWave / 4;
-#ifdef RHP_STAMPS
-    unsigned long long c0 = 0, c1 = 0;
-    RHP_STAMP(c0);
-#endif
+    dg.pass_begin();
     /* the deferred requests: the list finalize kept, or the whole range when
      * it overflowed */
     const uint32_t nd = *defer_n;
@@ -1467,9 +1496,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
                                       : http_frame_fast(p.bytes_rw + cur.off, cur.end - cur.off,
                                                         (int32_t) (cur.hint[1] & 0xffffu), &p.http[i], cur.hint[0],
                                                         cur.hint[2], cur.hint[3], p.hdrs + (uint64_t) i * p.hs_req, p.hs_hdr);
-#ifdef RHP_STAMPS
-      rp[3] += __popcll(__builtin_amdgcn_ballot_w64(fr == kFrameDone));
-#endif
+      dg.framed(fr == kFrameDone);
       if (fr != kFrameDone) {
         /* listed: the range-relative index, bit 31 = a chunked body to de-frame */
         const uint32_t at = atomicAdd(slow_n, 1u);
@@ -1479,36 +1506,20 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         else finish_slow(i, cur);
       }
     }
-#ifdef RHP_STAMPS
-    RHP_STAMP(c1);
-    rp[1] += c1 - c0;
-#endif
+    dg.pass_end(1);
     __syncthreads();
-#ifdef RHP_STAMPS
-    RHP_STAMP(c0);
-#endif
+    dg.pass_begin();
     const uint32_t ns = min(*slow_n, kSlowCap);
     for (uint32_t k = tid; k < ns; k += WAVES * 64) {
       const uint32_t e = slow[k], i = wg_lo + (e & 0x7fffffffu);
       const Head h = head(i);
       if (e >> 31) frame_chunked(p.bytes_rw + h.off, h.end - h.off, (int32_t) (h.hint[1] & 0xffffu), &p.http[i], p.compact);
       else finish_slow(i, h);
-#ifdef RHP_STAMPS
-      rp[2] += __popcll(__builtin_amdgcn_ballot_w64(true));
-#endif
+      dg.slow_path();
     }
-#ifdef RHP_STAMPS
-    RHP_STAMP(c1);
-    rp[0] += c1 - c0;
-#endif
+    dg.pass_end(0);
   }
-#ifdef RHP_STAMPS
-  if (lane == 0) {
-    const uint32_t w = (blockIdx.x * WAVES + (tid >> 6)) % 8192;
-    g_stamps[w * kStampSlots + 9] = __builtin_amdgcn_s_memrealtime();
-    for (int k = 0; k < 4; k++) g_stamps[w * kStampSlots + 15 + k] = rp[k];
-  }
-#endif
+  dg.exit(WAVES);
 }
 
 /* rhp_fixup_sessions: one thread per session (rhp_scalar.h fixup_session_t) */

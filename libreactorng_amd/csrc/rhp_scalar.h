@@ -507,7 +507,12 @@ RHP_HD void fixup_session_t(const FixupIO &io, uint32_t p_lo, uint32_t p_hi, uin
     while (j < p_hi && io.off[j] < pos) j++;
     rhp_http_t x;
     bool taken = false;
-    if (j < p_hi && io.off[j] == pos) {
+    /* piece j's speculative records are intact only while no earlier request
+     * of this walk has been written over them (slots below `slot` have): a
+     * piece that held more than one request -- a coarser split than the
+     * server's -- puts later boundaries behind `slot`, and those requests are
+     * parsed again from the true boundary */
+    if (j < p_hi && io.off[j] == pos && j >= slot) {
       x = io.http[j];
       const uint64_t plen = io.off[j + 1] - pos;
       taken = (x.result == 1 && x.consumed <= plen) || x.result == -1 || x.result == RHP_RET_TOOLONG ||

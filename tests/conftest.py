@@ -12,6 +12,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
 
 
+def pytest_report_header(config):
+    """the binaries this run tests, by content (committed logs tie results to them)"""
+    import libreactorng_amd as rhp
+    return [f"librhp.so sha256 {rhp.library_sha256()} ({rhp.LIBRHP})",
+            f"librhp_host.so sha256 {rhp.library_sha256(rhp.LIBHOST)}"]
+
+
 def _gpu_available() -> bool:
     try:
         import torch

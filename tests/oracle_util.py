@@ -128,29 +128,9 @@ def to_rhp(reqs, hdrs, http, mode):
 
 
 def canon(res: rhp.Result, mode):
-    """rhp.Result -> canonical records (fields unspecified by the reference zeroed)."""
-    reqs = res.reqs.copy()
-    n = len(reqs)
-    maxh = res.hdrs.shape[1] if res.hdrs.ndim == 2 else 0
-    ok = reqs["ret"] > 0
-    if mode == rhp.MODE_HTTP:
-        ok &= res.http["result"] == 1
-    for f in ("method_off", "method_len", "path_off", "path_len", "num_headers"):
-        reqs[f][~ok] = 0
-    reqs["minor_version"][~ok] = -1
-    reqs["flags"] = 0
-    h = res.hdrs.copy() if maxh else np.zeros((n, 0), dtype=rhp.HDR_DTYPE)
-    if maxh:
-        valid = ok[:, None] & (np.arange(maxh)[None, :] < reqs["num_headers"][:, None])
-        for f in h.dtype.names:
-            h[f] = np.where(valid, h[f], 0)
-    x = None
-    if mode == rhp.MODE_HTTP:
-        x = res.http.copy()
-        one = x["result"] == 1
-        for f in ("body_kind", "consumed", "body_len"):
-            x[f][~one] = 0
-    return reqs, h, x
+    """rhp.Result -> canonical records (fields unspecified by the reference zeroed):
+    rhp.canonical, the one bench.py's parity check uses too."""
+    return rhp.canonical(res, mode)
 
 
 def assert_same(got, want, buf=None, off=None, label=""):

@@ -132,6 +132,23 @@ def test_server_cases_gpu_batch_parser(writer, monkeypatch):
     assert "config1 16 pipelined   responses 16  callbacks 16" in out
 
 
+def test_server_thread_exit_host_async():
+    """A reactor thread serving with the asynchronous parser exits, three times
+    over: its parser state (the worker thread, slots, eventfd) is torn down by
+    the thread-exit hook, the worker joined before the state is freed."""
+    out = _run([os.path.join(BIN, "thread_exit_test")], "host-async")
+    assert "OK (0 failures)" in out and out.count("64 responses, exited") == 3
+
+
+@pytest.mark.gpu
+def test_server_thread_exit_gpu():
+    """The same with the MI355X parser: the completion waiter thread, the
+    round events, streams and pinned/device slots of an exiting reactor thread
+    are released, and each new thread sets up (and warms up) its own."""
+    out = _run([os.path.join(BIN, "thread_exit_test")], "gpu")
+    assert "OK (0 failures)" in out and out.count("64 responses, exited") == 3
+
+
 def test_reactor_host_code_asan_ubsan_clean(tmp_path):
     """libreactor.so, the host parser library and the two test programs built
     with -fsanitize=address,undefined (Makefile target `asan`): the reference's
@@ -142,7 +159,8 @@ def test_reactor_host_code_asan_ubsan_clean(tmp_path):
     asan = os.path.join(LIB, "asan")
     for args, parser in (([os.path.join(asan, "http_test"), _vectors(tmp_path)], "host"),
                          ([os.path.join(asan, "server_test"), "8", "16"], "host"),
-                         ([os.path.join(asan, "server_test"), "8", "16"], "host-async")):
+                         ([os.path.join(asan, "server_test"), "8", "16"], "host-async"),
+                         ([os.path.join(asan, "thread_exit_test")], "host-async")):
         p = subprocess.run(args, env=dict(env, RHP_REACTOR_PARSER=parser), capture_output=True, text=True, timeout=300)
         assert p.returncode == 0 and "OK (0 failures)" in p.stdout, p.stdout + p.stderr
         assert "runtime error" not in p.stderr and "AddressSanitizer" not in p.stderr, p.stderr

@@ -167,6 +167,34 @@ def test_fixup_cpu_unsplit_sessions():
     check(res, results, starts, buf, off, sess, "unsplit", allow_more=True)
 
 
+def merged_split(seed):
+    """A split coarser than the server's: runs of 1-3 consecutive server pieces
+    merged, so a piece may hold several requests and the walk meets request
+    boundaries inside pieces whose records an earlier request overwrote."""
+    rng = np.random.default_rng(seed)
+
+    def split(data):
+        p, out = rhp.split_pieces(data), []
+        while p:
+            k = int(rng.integers(1, 4))
+            out.append(sum(p[:k]))
+            p = p[k:]
+        return out
+    return split
+
+
+@pytest.mark.parametrize("emulate_dfa", [False, True])
+def test_fixup_cpu_partly_merged_split(emulate_dfa):
+    """Pieces that each hold up to three requests: requests past a
+    piece's first are parsed again from their true boundary, never read from
+    record slots the walk has already overwritten; sessions that run out of
+    pieces report `more`."""
+    data = make_sessions(80, 11)
+    buf, off, sess, _ = rhp.pack_sessions(data, split=merged_split(11))
+    res, results, starts = rhp.fixup_cpu(buf, off, sess, 16, emulate_dfa)
+    check(res, results, starts, buf, off, sess, "merged", allow_more=True)
+
+
 def test_fixup_cpu_every_chunking_of_one_stream():
     """One pipelined stream cut at every position into (delivered, rest): the
     delivered part as one session, as a server round sees a partial recv."""
@@ -197,6 +225,14 @@ def test_fixup_gpu_unsplit_sessions():
     res, results, starts = rhp.fixup_gpu(buf, off, sess)
     assert results["more"].sum() > 0
     check(res, results, starts, buf, off, sess, "gpu unsplit", allow_more=True)
+
+
+@pytest.mark.gpu
+def test_fixup_gpu_partly_merged_split():
+    data = make_sessions(300, 12)
+    buf, off, sess, _ = rhp.pack_sessions(data, split=merged_split(12))
+    res, results, starts = rhp.fixup_gpu(buf, off, sess)
+    check(res, results, starts, buf, off, sess, "gpu merged", allow_more=True)
 
 
 @pytest.mark.gpu

@@ -3,7 +3,7 @@
 # bench line, rocprofv3 kernel-trace summaries of configs 2/3/5 and PMC
 # FETCH_SIZE / WRITE_SIZE passes (separate runs).  Every GPU step has its own
 # time limit; steps are chained with && so a failure stops the session.
-# STEPS=tests,bench,prof,pmc,sq,writer,smoke (default all)
+# STEPS=tests,bench,prof,pmc,sq,writer,smoke,ceil (default all but ceil)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out && export TMPDIR=/tmp
 TAG=${TAG:-s}
@@ -44,9 +44,14 @@ step_writer() {
     && timeout -k 10 180 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_${TAG}_writer -o run \
       -- python3 tools/bench_writer.py > gpurun_out/prof_${TAG}_writer.log 2>&1 && echo WRITER_OK
 }
+step_ceil() {
+  # the read + record-write ceiling microbenchmark (built on the CPU beforehand), its ONLY_C forms
+  ONLY_C=1 timeout -k 10 180 tools/ubench_ceiling > gpurun_out/ceil_${TAG}.txt 2>&1 && cat gpurun_out/ceil_${TAG}.txt
+}
 step_smoke() {
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" > gpurun_out/smoke_${TAG}.log 2>&1 \
     && tail -1 gpurun_out/smoke_${TAG}.log
 }
 ( ! has tests || step_tests ) && ( ! has bench || step_bench ) && ( ! has prof || step_prof ) && ( ! has pmc || step_pmc ) \
-  && ( ! has sq || step_sq ) && ( ! has writer || step_writer ) && ( ! has smoke || step_smoke ) && echo SESSION_OK
+  && ( ! has sq || step_sq ) && ( ! has writer || step_writer ) && ( ! has smoke || step_smoke ) \
+  && ( ! has ceil || step_ceil ) && echo SESSION_OK

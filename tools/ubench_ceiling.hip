@@ -122,9 +122,29 @@ __global__ void group(const uint8_t *buf, uint8_t *reqs, uint8_t *hdrs, uint32_t
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
+/* a 16- / 4-byte global store with the sc1 bit: written through to memory,
+ * the line dropped from L2, so the launch leaves no dirty record lines for
+ * the kernel boundary's write-back (MI355X_MICROARCH.md, store flavours) */
+__device__ __forceinline__ void st16_wt(void *p, u32x4 v)
+{
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st8_wt(void *p, u32x2 v)
+{
+  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st4_wt(void *p, uint32_t v)
+{
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
 /* group with the records written in other forms: WM 1 = nt stores (ABI layout),
  * 2 = the wave's 3 KiB of records contiguous (tiled: reqs then the 4 header
- * runs of its 64 requests), 3 = reqs only (16 MB), 4 = headers only (32 MB) */
+ * runs of its 64 requests), 3 = reqs only (16 MB), 4 = headers only (32 MB),
+ * 5 = the ABI layout (48 B) with write-through (sc1) stores, 6 = compact
+ * records: 16-B request record + 4 x 4-B header records (u16 name_len, u16
+ * value_len) header-major, 32 B, 7 = 8-B request record + 4 x 4 B, 24 B,
+ * 8 / 9 = 6 / 7 with write-through stores */
 template <int U, int WM>
 __global__ void groupw(const uint8_t *buf, uint8_t *reqs, uint8_t *hdrs, uint32_t *out)
 {
@@ -158,6 +178,30 @@ __global__ void groupw(const uint8_t *buf, uint8_t *reqs, uint8_t *hdrs, uint32_
     } else if (WM == 4) {
 #pragma unroll
       for (int k = 0; k < 4; k++) *(gw2 *) (uintptr_t) (hdrs + 8 * ((uint64_t) k * kReqs + i)) = u32x2{acc, (uint32_t) k};
+    } else if (WM == 5) {
+      st16_wt(reqs + 16 * i, u32x4{acc, 1, 2, 3});
+#pragma unroll
+      for (int k = 0; k < 4; k++) st8_wt(hdrs + 8 * ((uint64_t) k * kReqs + i), u32x2{acc, (uint32_t) k});
+    } else if (WM == 6 || WM == 8) {
+      typedef __attribute__((address_space(1))) uint32_t gw1;
+      if (WM == 6) *(gw4 *) (uintptr_t) (reqs + 16 * i) = u32x4{acc, 1, 2, 3};
+      else st16_wt(reqs + 16 * i, u32x4{acc, 1, 2, 3});
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        uint8_t *q = hdrs + 4 * ((uint64_t) k * kReqs + i);
+        if (WM == 6) *(gw1 *) (uintptr_t) q = acc + k;
+        else st4_wt(q, acc + k);
+      }
+    } else if (WM == 7 || WM == 9) {
+      typedef __attribute__((address_space(1))) uint32_t gw1;
+      if (WM == 7) *(gw2 *) (uintptr_t) (reqs + 8 * i) = u32x2{acc, 1};
+      else st8_wt(reqs + 8 * i, u32x2{acc, 1});
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        uint8_t *q = hdrs + 4 * ((uint64_t) k * kReqs + i);
+        if (WM == 7) *(gw1 *) (uintptr_t) q = acc + k;
+        else st4_wt(q, acc + k);
+      }
     }
   }
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
@@ -262,6 +306,19 @@ int main()
 #define GROUPW(U, WM, GRID, BLOCK)                                                                              \
   run("groupw U" #U " wm" #WM " grid " #GRID "x" #BLOCK,                                                        \
       [&](uint8_t *in, uint32_t *) { hipLaunchKernelGGL((groupw<U, WM>), dim3(GRID), dim3(BLOCK), 0, 0, in, b.reqs, b.hdrs, b.out); }, b, false)
+  if (getenv("ONLY_C")) {   /* compact and write-through record forms (round 4) */
+    for (int rep = 0; rep < 2; rep++) {
+      GROUP(8, 1, 0, 256, 1024);
+      GROUP(8, 1, 1, 256, 1024);
+      GROUPW(8, 3, 256, 1024);
+      GROUPW(8, 5, 256, 1024);
+      GROUPW(8, 6, 256, 1024);
+      GROUPW(8, 7, 256, 1024);
+      GROUPW(8, 8, 256, 1024);
+      GROUPW(8, 9, 256, 1024);
+    }
+    return 0;
+  }
   if (getenv("ONLY_W")) {
     for (int rep = 0; rep < 2; rep++) {
       GROUP(8, 1, 0, 256, 1024);

@@ -50,7 +50,7 @@ sys.path.insert(0, ROOT)
 
 import libreactorng_amd as rhp  # noqa: E402
 
-LAYOUTS = {"request": rhp.LAYOUT_REQUEST_MAJOR, "header": rhp.LAYOUT_HEADER_MAJOR}
+LAYOUTS = {"request": rhp.LAYOUT_REQUEST_MAJOR, "header": rhp.LAYOUT_HEADER_MAJOR, "compact": rhp.LAYOUT_COMPACT}
 METRIC = "GiB/s device-resident batched HTTP/1.1 request parse, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E, GB/s (MI355X_MICROARCH.md chip table)
 CONFIGS = {
@@ -432,7 +432,10 @@ def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
     n_total = per_gpu * world
     lo, hi = shard_range(n_total, rank, world)
     alg_bytes = rhp.header_bytes(cfg["gen"], hi - lo, cfg["seed"], lo=lo)
-    layout = LAYOUTS[args.layout if args.layout != "auto" else cfg["layout"]]
+    # the compact records are a phr-mode layout (rhp.h): http configs keep their own under --layout compact
+    lay_name = cfg["layout"] if args.layout == "auto" or (args.layout == "compact" and cfg["mode"] != rhp.MODE_PHR) \
+        else args.layout
+    layout = LAYOUTS[lay_name]
     runner = (EmuRunner if args.device == "cpu" else GpuRunner)(cfg, lo, hi, args.copies, layout)
     for k in range(warmup):
         runner.step(k)
@@ -470,8 +473,7 @@ def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
             parity_entry["result"] = "match on the ranks with a reference digest" if any(int(c) == 0 for c in codes) \
                 else parity_entry["result"]
     return dict(cfg=cfg, lo=lo, hi=hi, n_total=n_total, alg_bytes=alg_bytes, total_alg=total_alg, wall=wall,
-                kern_ms=kern_ms, ok_frac=ok_frac, steps=steps, warmup=warmup, parity=parity_entry,
-                layout=args.layout if args.layout != "auto" else cfg["layout"])
+                kern_ms=kern_ms, ok_frac=ok_frac, steps=steps, warmup=warmup, parity=parity_entry, layout=lay_name)
 
 
 def roofline(r, key):

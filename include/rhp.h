@@ -60,6 +60,7 @@ typedef struct rhp_req {
 } rhp_req_t;
 
 #define RHP_F_EXACT 0x1u   /* resolved by the exact (scalar) device path, not the DFA */
+#define RHP_F_WIDE  0x2u   /* RHP_LAYOUT_COMPACT: this request's header records are the wide ones */
 
 /* struct phr_header as offsets (8 B); name_off == RHP_NAME_NULL encodes name ==
  * NULL (obs-fold continuation line, picohttpparser.c:318-321). */
@@ -79,8 +80,26 @@ typedef struct rhp_hdr {
  * profiles/r02/ubench_records.txt).  Records past num_headers are unspecified. */
 enum rhp_layout {
   RHP_LAYOUT_REQUEST_MAJOR = 0,
-  RHP_LAYOUT_HEADER_MAJOR = 1
+  RHP_LAYOUT_HEADER_MAJOR = 1,
+  RHP_LAYOUT_COMPACT = 2      /* RHP_MODE_PHR: 4-byte records, below */
 };
+/* Compact records (RHP_LAYOUT_COMPACT, RHP_MODE_PHR).  A header line the DFA
+ * parses is `name ": " value CRLF` and the first one starts right after the
+ * request line `method SP path SP "HTTP/1." digit CRLF`, so its record is two
+ * lengths: hdrs holds u32 lens[max_headers][n] (header-major), name_len |
+ * value_len << 16, and the offsets follow by a running sum,
+ *   name_off(0) = path_off + path_len + 11
+ *   value_off(k) = name_off(k) + name_len(k) + 2
+ *   name_off(k + 1) = value_off(k) + value_len(k) + 2.
+ * A request whose flags hold RHP_F_WIDE (the exact path parsed it: leading
+ * CRLF, OWS, obs-fold, bare LF, ...) has its records as rhp_hdr_t in the wide
+ * area, wide[n][max_headers] (request-major) at byte RHP_COMPACT_WIDE_OFF(n, m)
+ * of hdrs.  hdrs holds RHP_COMPACT_HDRS_BYTES(n, m) bytes; rhp_expand_records
+ * (rhp_host.h) turns a batch's records into rhp_hdr_t on the host.  The
+ * records a uniform batch writes shrink from 8 to 4 bytes per header (config
+ * 2: 48 -> 32 B per request with the 16-B request record). */
+#define RHP_COMPACT_WIDE_OFF(n, m) ((((size_t) (n) * (size_t) (m) * 4u) + 15u) & ~(size_t) 15u)
+#define RHP_COMPACT_HDRS_BYTES(n, m) (RHP_COMPACT_WIDE_OFF(n, m) + (size_t) (n) * (size_t) (m) * 8u)
 /* record k of request i in a batch of n requests with capacity m */
 #define RHP_HDR(hdrs, layout, n, m, i, k) \
   ((hdrs)[(layout) == RHP_LAYOUT_HEADER_MAJOR ? (size_t) (k) * (n) + (i) : (size_t) (i) * (m) + (k)])
@@ -108,7 +127,8 @@ typedef struct rhp_batch {
   uint32_t        layout;      /* enum rhp_layout: where record k of request i lives in hdrs */
   rhp_req_t      *reqs;        /* device [n] */
   rhp_hdr_t      *hdrs;        /* device [n * max_headers] records, laid out as `layout` says
-                                  (n * max_headers < 2^32) */
+                                  (n * max_headers < 2^32); RHP_LAYOUT_COMPACT:
+                                  RHP_COMPACT_HDRS_BYTES(n, max_headers) bytes */
   rhp_http_t     *http;        /* device [n], RHP_MODE_HTTP */
   uint32_t       *work;        /* reserved, may be NULL (device scratch of RHP_WORK_WORDS u32
                                   for future kernels; the current ones keep their scheduling

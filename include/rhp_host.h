@@ -8,6 +8,8 @@
  *   rhp_emu_parse_batch   CPU emulation of the kernel's DFA algorithm, block for
  *                         block (tests only); stats[3] = fast ok, fast -1, exact
  *   (both take an rhp_batch_t (include/rhp.h) whose pointers are host memory)
+ *   rhp_expand_records    any layout's header records (the compact ones
+ *                         included) as rhp_hdr_t, on the host
  *
  *   rhp_phr_parse_request the same exact parser with phr_parse_request's own
  *                         signature and outputs (pointers into buf, no length
@@ -35,6 +37,14 @@ int rhp_cpu_parse_batch(const rhp_batch_t *batch);
 int rhp_cpu_fixup_sessions(const rhp_batch_t *batch, const rhp_session_t *sessions, uint32_t n_sessions,
                            rhp_session_result_t *results, uint64_t *req_start);
 int rhp_emu_parse_batch(const rhp_batch_t *batch, uint64_t *stats);
+
+/* A parsed batch's header records as rhp_hdr_t, out[i * max_headers + k]
+ * (request-major), from host copies of its reqs and hdrs in the batch's
+ * layout; records past num_headers and those of requests with ret <= 0 are
+ * zeroed.  For RHP_LAYOUT_COMPACT this is the running sum of rhp.h (the wide
+ * records for RHP_F_WIDE requests).  `batch` supplies n, max_headers and
+ * layout only.  0, or -22 on bad arguments. */
+int rhp_expand_records(const rhp_batch_t *batch, const rhp_req_t *reqs, const void *hdrs, rhp_hdr_t *out);
 
 /* struct phr_header (picohttpparser.h:42-47): name == NULL for an obs-fold line */
 typedef struct rhp_phr_header {

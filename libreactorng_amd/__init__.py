@@ -27,10 +27,11 @@ RHP_MAX_HEADERS = 64
 RHP_RET_TOOLONG = -3
 RHP_WORK_WORDS = 64
 MODE_PHR, MODE_HTTP = 0, 1
-LAYOUT_REQUEST_MAJOR, LAYOUT_HEADER_MAJOR = 0, 1
+LAYOUT_REQUEST_MAJOR, LAYOUT_HEADER_MAJOR, LAYOUT_COMPACT = 0, 1, 2
 IMPL_DFA, IMPL_EXACT, IMPL_DFA_LATE = 0, 1, 2
 RHP_NAME_NULL = 0xFFFF
 F_EXACT = 0x1
+F_WIDE = 0x2   # compact layout: the request's header records are in the wide area (rhp.h)
 
 GEN_TFB128, GEN_GET256, GEN_ZIPF, GEN_POST1K, GEN_CHUNKED, GEN_FUZZ, GEN_FUZZ_HTTP = 1, 2, 3, 5, 6, 100, 101
 
@@ -63,7 +64,7 @@ RHP_SYMBOLS = ("rhp_parse_batch", "rhp_set_impl", "rhp_kernel_name", "rhp_versio
                "rhp_fixup_sessions")
 HOST_SYMBOLS = ("rhp_gen_size", "rhp_gen_fill", "rhp_gen_header_bytes", "rhp_splitmix64",
                 "rhp_emu_parse_batch", "rhp_cpu_parse_batch", "rhp_phr_parse_request", "rhp_http_read_cpu",
-                "rhp_cpu_fixup_sessions")
+                "rhp_cpu_fixup_sessions", "rhp_expand_records")
 
 _rhp = None
 _host = None
@@ -125,6 +126,8 @@ def host() -> ctypes.CDLL:
         _host.rhp_http_read_cpu.restype = ctypes.c_int
         _host.rhp_cpu_fixup_sessions.argtypes = [ctypes.POINTER(Batch), vp, ctypes.c_uint32, vp, vp]
         _host.rhp_cpu_fixup_sessions.restype = ctypes.c_int
+        _host.rhp_expand_records.argtypes = [ctypes.POINTER(Batch), vp, vp, vp]
+        _host.rhp_expand_records.restype = ctypes.c_int
     return _host
 
 
@@ -201,9 +204,11 @@ def header_bytes(config: int, n: int, seed: int, lo: int = 0) -> int:
 @dataclass
 class Result:
     reqs: np.ndarray           # REQ_DTYPE [n]
-    hdrs: np.ndarray           # HDR_DTYPE [n, max_headers] (a view of the header-major batch array)
+    hdrs: np.ndarray           # HDR_DTYPE [n, max_headers] (a view of the header-major batch array; the
+    #                            compact layout's records expanded by rhp_expand_records)
     http: np.ndarray | None    # HTTP_DTYPE [n] (http mode)
     bytes_out: np.ndarray | None = None  # request bytes after http mode (chunked bodies rewritten)
+    raw_hdrs: np.ndarray | None = None   # the hdrs buffer as the parser left it (its layout's bytes)
 
 
 def canonical(res: Result, mode: int):
@@ -257,6 +262,29 @@ def library_sha256(path: str | None = None) -> str:
     return hashlib.sha256(open(p, "rb").read()).hexdigest()
 
 
+def hdrs_bytes(n: int, max_headers: int, layout: int) -> int:
+    """bytes the batch's hdrs buffer needs (rhp.h; RHP_COMPACT_HDRS_BYTES for the compact layout)"""
+    if layout == LAYOUT_COMPACT:
+        return ((n * max_headers * 4 + 15) & ~15) + n * max_headers * HDR_DTYPE.itemsize
+    return n * max_headers * HDR_DTYPE.itemsize
+
+
+def expand_records(reqs: np.ndarray, raw: np.ndarray, n: int, max_headers: int, layout: int) -> np.ndarray:
+    """[n, max_headers] rhp_hdr_t records of a parsed batch from its raw hdrs bytes
+    in any layout (rhp_expand_records, include/rhp_host.h): records of requests
+    with ret <= 0 and past num_headers are zero."""
+    out = np.zeros((n, max_headers), dtype=HDR_DTYPE)
+    if n == 0 or max_headers == 0:
+        return out
+    reqs = np.ascontiguousarray(reqs)
+    raw = np.ascontiguousarray(raw).view(np.uint8)
+    b = Batch(None, None, None, 0, n, max_headers, MODE_PHR, layout, None, None, None, None, 0, 0, None)
+    rc = host().rhp_expand_records(ctypes.byref(b), _ptr(reqs), _ptr(raw), _ptr(out))
+    if rc != 0:
+        raise RuntimeError(f"rhp_expand_records failed: {rc}")
+    return out
+
+
 def hdr_view(flat: np.ndarray, n: int, max_headers: int, layout: int) -> np.ndarray:
     """The [n, max_headers] view of a batch's record array in either layout (include/rhp.h)."""
     if layout == LAYOUT_HEADER_MAJOR:
@@ -267,12 +295,21 @@ def hdr_view(flat: np.ndarray, n: int, max_headers: int, layout: int) -> np.ndar
 def _host_batch(buf, off, max_headers, mode, layout=LAYOUT_REQUEST_MAJOR, last_len=None, flags=0):
     n = len(off) - 1
     reqs = np.zeros(n, dtype=REQ_DTYPE)
-    hdrs = np.zeros(max(max_headers * n, 1), dtype=HDR_DTYPE)
+    raw = np.zeros(max(hdrs_bytes(n, max_headers, layout), 8), dtype=np.uint8)
     http = np.zeros(n, dtype=HTTP_DTYPE)
     rw = buf.copy()
-    b = Batch(_ptr(rw), _ptr(rw), _ptr(off), rw.size, n, max_headers, mode, layout, _ptr(reqs), _ptr(hdrs),
+    b = Batch(_ptr(rw), _ptr(rw), _ptr(off), rw.size, n, max_headers, mode, layout, _ptr(reqs), _ptr(raw),
               _ptr(http), 0, flags, 0, _ptr(last_len) if last_len is not None else None)
-    return b, Result(reqs, hdr_view(hdrs, n, max_headers, layout), http if mode == MODE_HTTP else None, rw)
+    hv = None if layout == LAYOUT_COMPACT else hdr_view(raw.view(HDR_DTYPE), n, max_headers, layout)
+    res = Result(reqs, hv, http if mode == MODE_HTTP else None, rw)
+    res.raw_hdrs = raw   # the compact layout's records are expanded once the parse has run (_host_done)
+    return b, res
+
+
+def _host_done(res: Result, n: int, max_headers: int, layout: int) -> Result:
+    if layout == LAYOUT_COMPACT:
+        res.hdrs = expand_records(res.reqs, res.raw_hdrs, n, max_headers, layout)
+    return res
 
 
 def emulate(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,
@@ -286,15 +323,17 @@ def emulate(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int =
     rc = host().rhp_emu_parse_batch(ctypes.byref(b), _ptr(stats))
     if rc != 0:
         raise RuntimeError(f"rhp_emu_parse_batch failed: {rc}")
-    return res, stats
+    return _host_done(res, len(off) - 1, max_headers, layout), stats
 
 
 def parse_cpu_exact(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,
                     layout: int = LAYOUT_REQUEST_MAJOR):
     """The product's exact scalar parser on the host (rhp_scalar.h), e.g. for the reactor shim."""
     b, res = _host_batch(buf, off, max_headers, mode, layout)
-    host().rhp_cpu_parse_batch(ctypes.byref(b))
-    return res
+    rc = host().rhp_cpu_parse_batch(ctypes.byref(b))
+    if rc != 0:
+        raise RuntimeError(f"rhp_cpu_parse_batch failed: {rc}")
+    return _host_done(res, len(off) - 1, max_headers, layout)
 
 
 class DeviceBatch:
@@ -314,8 +353,7 @@ class DeviceBatch:
         self.bytes = torch.from_numpy(buf).to(device)
         self.offsets = torch.from_numpy(off.view(np.int64)).to(device)
         self.reqs = torch.zeros(self.n * REQ_DTYPE.itemsize, dtype=torch.uint8, device=device)
-        self.hdrs = torch.zeros(max(self.n * max_headers, 1) * HDR_DTYPE.itemsize, dtype=torch.uint8,
-                                device=device)
+        self.hdrs = torch.zeros(max(hdrs_bytes(self.n, max_headers, layout), 8), dtype=torch.uint8, device=device)
         self.http = torch.zeros((self.n if mode == MODE_HTTP else 1) * HTTP_DTYPE.itemsize, dtype=torch.uint8,
                                 device=device)
         self.work = torch.zeros(RHP_WORK_WORDS, dtype=torch.int32, device=device)
@@ -340,10 +378,12 @@ class DeviceBatch:
         import torch
         torch.cuda.synchronize()
         reqs = self.reqs.cpu().numpy().view(REQ_DTYPE)
-        hdrs = hdr_view(self.hdrs.cpu().numpy().view(HDR_DTYPE), self.n, self.max_headers, self.layout)
+        raw = self.hdrs.cpu().numpy()
+        hdrs = (expand_records(reqs, raw, self.n, self.max_headers, self.layout) if self.layout == LAYOUT_COMPACT
+                else hdr_view(raw.view(HDR_DTYPE), self.n, self.max_headers, self.layout))
         http = self.http.cpu().numpy().view(HTTP_DTYPE) if self.mode == MODE_HTTP else None
         out = self.bytes.cpu().numpy() if self.mode == MODE_HTTP else None
-        return Result(reqs, hdrs, http, out)
+        return Result(reqs, hdrs, http, out, raw)
 
 
 def parse_batch(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,

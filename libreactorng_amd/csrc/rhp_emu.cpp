@@ -31,13 +31,26 @@ struct Stats {
   uint64_t fast_ok, fast_bad, exact;
 };
 
+/* the exact path's (wide) records of request i: the batch's hdrs in its layout,
+ * or the wide area behind the lengths of a compact batch (rhp.h) */
+rhp_hdr_t *wide_records(const rhp_batch_t *b, uint32_t i, uint64_t &hs_hdr)
+{
+  if (b->layout == RHP_LAYOUT_COMPACT) {
+    hs_hdr = 1u;
+    return reinterpret_cast<rhp_hdr_t *>(reinterpret_cast<uint8_t *>(b->hdrs) + RHP_COMPACT_WIDE_OFF(b->n, b->max_headers)) +
+           (uint64_t) i * b->max_headers;
+  }
+  const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR;
+  hs_hdr = hmajor ? b->n : 1u;
+  return b->hdrs + (uint64_t) i * (hmajor ? 1u : b->max_headers);
+}
+
 void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
 {
   rhp_req_t r;
-  r.flags = RHP_F_EXACT;
-  const uint64_t hs_req = b->layout == RHP_LAYOUT_HEADER_MAJOR ? 1u : b->max_headers;
-  const uint64_t hs_hdr = b->layout == RHP_LAYOUT_HEADER_MAJOR ? b->n : 1u;
-  rhp_hdr_t *h = b->hdrs + i * hs_req;
+  r.flags = RHP_F_EXACT | (b->layout == RHP_LAYOUT_COMPACT ? RHP_F_WIDE : 0u);
+  uint64_t hs_hdr = 1;
+  rhp_hdr_t *h = wide_records(b, i, hs_hdr);
   if (b->mode == RHP_MODE_HTTP) {
     PlainBytes B{b->bytes_rw + off};
     scalar_http_t(B, b->bytes_rw + off, len, b->max_headers, &r, h, hs_hdr, &b->http[i],
@@ -50,7 +63,7 @@ void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
       memset(&r, 0, sizeof r);
       r.ret = pre;
       r.minor_version = -1;
-      r.flags = RHP_F_EXACT;
+      r.flags = RHP_F_EXACT | (b->layout == RHP_LAYOUT_COMPACT ? RHP_F_WIDE : 0u);
     } else {
       scalar_phr(b->bytes + off, len, b->max_headers, &r, h, hs_hdr);
     }
@@ -62,6 +75,7 @@ void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
 
 extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] or NULL */)
 {
+  if (b->layout == RHP_LAYOUT_COMPACT && b->mode != RHP_MODE_PHR) return -22;   /* as rhp_parse_batch */
   const Table2 &T = table();
   const uint8_t *cls = T.b + kClassRow * 256u;
   Stats st_count = {0, 0, 0};
@@ -76,9 +90,11 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
     uint32_t st = idx2(s0, 0);
     Dec d;
     dec_reset(d);
+    const bool compact = b->layout == RHP_LAYOUT_COMPACT;
     const uint64_t hs_req = b->layout == RHP_LAYOUT_HEADER_MAJOR ? 1u : maxh;
     const uint64_t hs_hdr = b->layout == RHP_LAYOUT_HEADER_MAJOR ? b->n : 1u;
-    rhp_hdr_t *hout = b->hdrs + i * hs_req;
+    rhp_hdr_t *hout = compact ? nullptr : b->hdrs + i * hs_req;
+    uint32_t *lens = compact ? reinterpret_cast<uint32_t *>(b->hdrs) + i : nullptr;   /* lens[k * n + i] */
     for (;;) {
       /* one RHP_BLOCK-byte block: steps, then the decode of its event mask */
       const int32_t block_pos = pos;
@@ -112,11 +128,15 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
           m &= m - 1;
           uint32_t lo, hi;
           if (dec_event(d, (uint32_t) (block_pos + 64 * w) + bit, maxh, lo, hi)) {
-            rhp_hdr_t &o = hout[(uint64_t) (d.nh - 1) * hs_hdr];
-            o.name_off = (uint16_t) lo;
-            o.name_len = (uint16_t) (lo >> 16);
-            o.value_off = (uint16_t) hi;
-            o.value_len = (uint16_t) (hi >> 16);
+            if (compact) {   /* as the kernel: the two lengths (rhp.h RHP_LAYOUT_COMPACT) */
+              lens[(uint64_t) (d.nh - 1) * b->n] = (lo >> 16) | (hi & 0xffff0000u);
+            } else {
+              rhp_hdr_t &o = hout[(uint64_t) (d.nh - 1) * hs_hdr];
+              o.name_off = (uint16_t) lo;
+              o.name_len = (uint16_t) (lo >> 16);
+              o.value_off = (uint16_t) hi;
+              o.value_len = (uint16_t) (hi >> 16);
+            }
           }
         }
       }
@@ -172,6 +192,37 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
   return 0;
 }
 
+extern "C" int rhp_expand_records(const rhp_batch_t *b, const rhp_req_t *reqs, const void *hdrs, rhp_hdr_t *out)
+{
+  if (!b || !reqs || !out || (b->max_headers && !hdrs)) return -22;
+  const uint32_t n = b->n, m = b->max_headers;
+  const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR, compact = b->layout == RHP_LAYOUT_COMPACT;
+  if (!hmajor && !compact && b->layout != RHP_LAYOUT_REQUEST_MAJOR) return -22;
+  const rhp_hdr_t *h = static_cast<const rhp_hdr_t *>(hdrs);
+  const uint32_t *lens = static_cast<const uint32_t *>(hdrs);
+  const rhp_hdr_t *wide =
+      reinterpret_cast<const rhp_hdr_t *>(static_cast<const uint8_t *>(hdrs) + RHP_COMPACT_WIDE_OFF(n, m));
+  for (uint32_t i = 0; i < n; i++) {
+    rhp_hdr_t *o = out + (uint64_t) i * m;
+    memset(o, 0, sizeof(rhp_hdr_t) * m);
+    const rhp_req_t &r = reqs[i];
+    if (r.ret <= 0) continue;
+    const uint32_t nh = r.num_headers < m ? r.num_headers : m;
+    if (compact && !(r.flags & RHP_F_WIDE)) {
+      uint32_t at = (uint32_t) r.path_off + r.path_len + 11u;   /* the first header line (rhp.h) */
+      for (uint32_t k = 0; k < nh; k++) {
+        const uint32_t l = lens[(uint64_t) k * n + i], nl = l & 0xffffu, vl = l >> 16;
+        o[k] = rhp_hdr_t{(uint16_t) at, (uint16_t) nl, (uint16_t) (at + nl + 2u), (uint16_t) vl};
+        at += nl + vl + 4u;
+      }
+    } else {
+      for (uint32_t k = 0; k < nh; k++)
+        o[k] = compact ? wide[(uint64_t) i * m + k] : hmajor ? h[(uint64_t) k * n + i] : h[(uint64_t) i * m + k];
+    }
+  }
+  return 0;
+}
+
 /* rhp_fixup_sessions (rhp.h) on the host: the same walk (rhp_scalar.h
  * fixup_session_t) over a speculative batch parsed by rhp_cpu_parse_batch or
  * rhp_emu_parse_batch. */
@@ -191,6 +242,7 @@ extern "C" int rhp_cpu_fixup_sessions(const rhp_batch_t *b, const rhp_session_t 
 /* The exact scalar path alone, on the host (the product's CPU parser). */
 extern "C" int rhp_cpu_parse_batch(const rhp_batch_t *b)
 {
+  if (b->layout == RHP_LAYOUT_COMPACT && b->mode != RHP_MODE_PHR) return -22;   /* as rhp_parse_batch */
   for (uint32_t i = 0; i < b->n; i++) emu_exact(b, i, b->offsets[i], b->offsets[i + 1] - b->offsets[i]);
   return 0;
 }

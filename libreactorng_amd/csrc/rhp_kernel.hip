@@ -60,8 +60,13 @@ struct Params {
   uint32_t max_headers;
   uint32_t mode;
   uint32_t span;    /* requests per workgroup */
-  uint32_t hs_req;  /* record stride between requests (rhp_layout) */
+  uint32_t hs_req;  /* stride of the exact path's rhp_hdr_t records between requests (rhp_layout) */
   uint32_t hs_hdr;  /* ... between the records of one request */
+  /* the records the DFA writes: rhp_hdr_t at hdrs, or (RHP_LAYOUT_COMPACT) u32
+   * lengths at lens, header-major, the exact path's records then in the wide
+   * area at hdrs */
+  uint32_t *lens;
+  uint32_t rec_req, rec_hdr;
 };
 
 #ifndef RHP_WAVES_PER_SIMD
@@ -356,7 +361,7 @@ struct DevDechunk {
 __device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64_t off, uint64_t len)
 {
   rhp_req_t r;
-  r.flags = RHP_F_EXACT;
+  r.flags = RHP_F_EXACT | (p.lens ? RHP_F_WIDE : 0u);   /* compact layout: this request's records are wide */
   rhp_hdr_t *h = p.hdrs + (uint64_t) i * p.hs_req;
   if (p.mode == RHP_MODE_HTTP) {
     rhp_http_t x;
@@ -547,6 +552,13 @@ __device__ __forceinline__ uint32_t lds_u8(uint32_t a)
 /* keep the compiler from sinking the computation of x into a branch */
 __device__ __forceinline__ void opaque(uint32_t &x) { asm("" : "+v"(x)); }
 
+/* The loop's record stores are write-through (sc1): the line goes to memory
+ * and leaves L2, so a launch ends with no dirty record lines for the kernel
+ * boundary's L2 write-back to drain (MI355X_MICROARCH.md, store flavours and
+ * the boundary row).  Measured on config 2's shape (tools/ubench_ceiling.hip,
+ * profiles/r04/a/ceil_r4a.txt): read + 48 B of records per request 53.9 us
+ * with plain stores, 52.1 us write-through. */
+
 /* one header record (8 B) for the lanes in `mask` (a ballot), as straight-line
  * code: exec is restored before the asm ends; the trailing s_nop covers the
  * store-data read hazard */
@@ -555,37 +567,52 @@ __device__ __forceinline__ void store_rec_lanes(uint64_t mask, rhp_hdr_t *dst, u
   uint64_t saved;
   asm volatile("s_mov_b64 %0, exec\n\t"
                "s_mov_b64 exec, %1\n\t"
-               "global_store_dwordx2 %2, %3, off\n\t"
+               "global_store_dwordx2 %2, %3, off sc1\n\t"
                "s_mov_b64 exec, %0\n\t"
                "s_nop 1"
                : "=&s"(saved)
                : "s"(mask), "v"(dst), "v"(v)
                : "memory");
 }
-__device__ __forceinline__ void store_req(rhp_req_t *dst, const rhp_req_t &r)
+/* the same for a compact header record (RHP_LAYOUT_COMPACT: name_len |
+ * value_len << 16) */
+__device__ __forceinline__ void store_len_lanes(uint64_t mask, uint32_t *dst, uint32_t v)
 {
-  u32x4 v;
-  __builtin_memcpy(&v, &r, sizeof r);
-  *GLOBAL(u32x4, dst) = v;
+  uint64_t saved;
+  asm volatile("s_mov_b64 %0, exec\n\t"
+               "s_mov_b64 exec, %1\n\t"
+               "global_store_dword %2, %3, off sc1\n\t"
+               "s_mov_b64 exec, %0\n\t"
+               "s_nop 1"
+               : "=&s"(saved)
+               : "s"(mask), "v"(dst), "v"(v)
+               : "memory");
+}
+/* 16 / 8 bytes, write-through, for the active lanes */
+__device__ __forceinline__ void store16_wt(void *dst, u32x4 v)
+{
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
+}
+__device__ __forceinline__ void store8_wt(void *dst, u32x2 v)
+{
+  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
 }
 __device__ __forceinline__ void store_http(rhp_http_t *dst, const rhp_http_t &x)
 {
-  typedef uint32_t u32x2a8 __attribute__((ext_vector_type(2), aligned(8)));
-  u32x2a8 v[3];
+  u32x2 v[3];
   __builtin_memcpy(v, &x, sizeof x);
-  __attribute__((address_space(1))) u32x2a8 *q = GLOBAL(u32x2a8, dst);
-  q[0] = v[0];
-  q[1] = v[1];
-  q[2] = v[2];
+  uint8_t *q = reinterpret_cast<uint8_t *>(dst);
+  store8_wt(q, v[0]);
+  store8_wt(q + 8, v[1]);
+  store8_wt(q + 16, v[2]);
 }
 __device__ __forceinline__ void store_http_bad(rhp_http_t *dst)
 {
   /* {result -1, body_kind 0, consumed 0, body_len 0} */
-  typedef uint32_t u32x2a8 __attribute__((ext_vector_type(2), aligned(8)));
-  __attribute__((address_space(1))) u32x2a8 *q = GLOBAL(u32x2a8, dst);
-  q[0] = u32x2a8{0xffffffffu, 0u};
-  q[1] = u32x2a8{0u, 0u};
-  q[2] = u32x2a8{0u, 0u};
+  uint8_t *q = reinterpret_cast<uint8_t *>(dst);
+  store8_wt(q, u32x2{0xffffffffu, 0u});
+  store8_wt(q + 8, u32x2{0u, 0u});
+  store8_wt(q + 16, u32x2{0u, 0u});
 }
 
 }  // namespace
@@ -599,7 +626,7 @@ __device__ __forceinline__ void store_http_bad(rhp_http_t *dst)
  * events of the window walked in the previous iteration) -- the same request
  * unless the lane switched between the two windows.
  */
-template <int WAVES, bool LATE, bool HTTP>
+template <int WAVES, bool LATE, bool HTTP, bool COMPACT>
 __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel(Params p)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -846,7 +873,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         const uint32_t e = base + (uint32_t) __builtin_ctz(eolm | 0x80000000u);
         const uint32_t co = t ? pco : base + (uint32_t) __builtin_ctz(com | 0x80000000u);
         const uint32_t lo = ls | ((co - ls) << 16), hi = (co + 2u) | ((e - co - 3u) << 16);
-        store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi});
+        if constexpr (COMPACT) store_len_lanes(st_m, p.lens + hx, (co - ls) | ((e - co - 3u) << 16));
+        else store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi});
         if (http) {   /* uniform: framing candidates only in http mode */
           const uint32_t nlen = co - ls;
           const bool cnd = has && (nlen == 14u || nlen == 17u);
@@ -859,7 +887,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         eolm &= eolm - 1u;
         ls = has ? e + 1u : ls;
         nh += (uint32_t) has;
-        hx += has ? p.hs_hdr : 0u;
+        hx += has ? p.rec_hdr : 0u;
         t = has ? 0u : t;
       }
       /* a colon left open at the end of the word: a later word (or window) has its LF */
@@ -878,7 +906,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const bool rec = has && !stop;
       const uint32_t lo = ls | ((co - ls) << 16), hi = (co + 2u) | ((e - co - 3u) << 16);
       const uint64_t st_m = __builtin_amdgcn_ballot_w64(rec);
-      if (st_m) store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi});
+      if (st_m) {
+        if constexpr (COMPACT) store_len_lanes(st_m, p.lens + hx, (co - ls) | ((e - co - 3u) << 16));
+        else store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi});
+      }
       if (http) {
         const uint32_t nlen = co - ls;
         const bool cnd = rec && (nlen == 14u || nlen == 17u);
@@ -893,7 +924,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       eolm = stop ? 0u : rec ? eolm & (eolm - 1u) : eolm;
       ls = rec ? e + 1u : ls;
       nh += rec ? 1u : 0u;
-      hx += rec ? p.hs_hdr : 0u;
+      hx += rec ? p.rec_hdr : 0u;
       t = rec ? 0u : t;
     }
     const bool open = com != 0;
@@ -1031,7 +1062,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     for (int q = 0; q < (int) kEvWords; q++) mq[q] = evp[q] & live;
     term_pos = 0xffffffffu;
     dstop = 0;
-    hx = dcur * p.hs_req + nh * p.hs_hdr;
+    hx = dcur * p.rec_req + nh * p.rec_hdr;
     if (term_ev) {   /* the terminal is the window's last event: take it off the mask */
       const int q = mq[3] ? 3 : mq[2] ? 2 : mq[1] ? 1 : 0;
       uint32_t w = q == 3 ? mq[3] : q == 2 ? mq[2] : q == 1 ? mq[1] : mq[0];
@@ -1109,8 +1140,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         }
         if (!framed) {
           defer(dcur);
-          typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-          *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{cand, kHintFrame | (term_pos + 1u), crec_lo, crec_hi};
+          store16_wt(&p.http[dcur], u32x4{cand, kHintFrame | (term_pos + 1u), crec_lo, crec_hi});
         }
       }
     } else if (bad) {
@@ -1119,12 +1149,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     } else {
       rq[3] = (uint32_t) kDeferExact << 16;   /* exact path: replay */
       defer(dcur);
-      if (http) {
-        typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-        *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{0u, kHintExact, 0u, 0u};
-      }
+      if (http) store16_wt(&p.http[dcur], u32x4{0u, kHintExact, 0u, 0u});
     }
-    *GLOBAL(u32x4, p.reqs + dcur) = rq;
+    store16_wt(p.reqs + dcur, rq);
     dhas = false;
     return true;
   };
@@ -1551,7 +1578,7 @@ namespace {
  * the implementation choice (rhp_set_impl, diagnostics) is per thread. */
 constexpr int kMaxDevices = 64;
 std::atomic<int> g_cus[kMaxDevices];
-std::atomic<uint32_t> g_attr[kMaxDevices];   /* bit 4(w/4)+2late+http: the LDS attribute of rhp_dfa_kernel<w, late, http> is set */
+std::atomic<uint64_t> g_attr[kMaxDevices];   /* bit 8(w/4)+4compact+2late+http: the LDS attribute of rhp_dfa_kernel<w, late, http, compact> is set */
 thread_local int t_impl = RHP_IMPL_DFA;
 
 int device_cus(int dev, int *cus)
@@ -1566,14 +1593,14 @@ int device_cus(int dev, int *cus)
   return 0;
 }
 
-template <int WAVES, bool LATE, bool HTTP>
+template <int WAVES, bool LATE, bool HTTP, bool COMPACT>
 int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
 {
   const size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes;
-  const uint32_t bit = 1u << (4 * (WAVES / 4) + (LATE ? 2 : 0) + (HTTP ? 1 : 0));
+  const uint64_t bit = 1ull << (8 * (WAVES / 4) + (COMPACT ? 4 : 0) + (LATE ? 2 : 0) + (HTTP ? 1 : 0));
   if (!(g_attr[dev].load(std::memory_order_acquire) & bit)) {
     /* idempotent: two threads of one device may both set it */
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES, LATE, HTTP>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES, LATE, HTTP, COMPACT>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds_bytes);
     if (e != hipSuccess) return (int) e;
     g_attr[dev].fetch_or(bit, std::memory_order_release);
@@ -1585,7 +1612,7 @@ int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
   /* each workgroup owns a contiguous n/grid share of the requests */
   Params q = prm;
   q.span = (prm.n + grid - 1) / grid;
-  hipLaunchKernelGGL((rhp_dfa_kernel<WAVES, LATE, HTTP>), dim3(grid), dim3(WAVES * 64), lds_bytes, s, q);
+  hipLaunchKernelGGL((rhp_dfa_kernel<WAVES, LATE, HTTP, COMPACT>), dim3(grid), dim3(WAVES * 64), lds_bytes, s, q);
   return (int) hipGetLastError();
 }
 
@@ -1633,7 +1660,8 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   if ((uint64_t) b->n * b->max_headers > 0xffffffffull) return -22;   /* record indices are 32-bit */
   if (b->mode == RHP_MODE_HTTP && (!b->http || !b->bytes_rw)) return -22;
   if (b->mode != RHP_MODE_PHR && b->mode != RHP_MODE_HTTP) return -22;
-  if (b->layout != RHP_LAYOUT_REQUEST_MAJOR && b->layout != RHP_LAYOUT_HEADER_MAJOR) return -22;
+  if (b->layout != RHP_LAYOUT_REQUEST_MAJOR && b->layout != RHP_LAYOUT_HEADER_MAJOR &&
+      !(b->layout == RHP_LAYOUT_COMPACT && b->mode == RHP_MODE_PHR)) return -22;   /* compact: phr mode */
   if (b->last_len && b->mode != RHP_MODE_PHR) return -22;   /* http_read_request passes last_len 0 */
   if ((b->flags & ~RHP_BATCH_SPECULATIVE) || ((b->flags & RHP_BATCH_SPECULATIVE) && b->mode != RHP_MODE_HTTP)) return -22;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -1660,8 +1688,18 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.mode = b->mode;
   prm.span = 0;
   const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR;
+  const bool compact = b->layout == RHP_LAYOUT_COMPACT;
   prm.hs_req = hmajor ? 1u : b->max_headers;
   prm.hs_hdr = hmajor ? b->n : 1u;
+  prm.lens = nullptr;
+  prm.rec_req = prm.hs_req;
+  prm.rec_hdr = prm.hs_hdr;
+  if (compact) {   /* lengths header-major at hdrs, the wide records request-major behind them */
+    prm.lens = reinterpret_cast<uint32_t *>(b->hdrs);
+    prm.hdrs = reinterpret_cast<rhp_hdr_t *>(reinterpret_cast<uint8_t *>(b->hdrs) + RHP_COMPACT_WIDE_OFF(b->n, b->max_headers));
+    prm.rec_req = 1u;
+    prm.rec_hdr = b->n;
+  }
 
   /* the DFA kernel addresses windows with u32 offsets from its workgroup's
    * range start; a range of ~4 GiB runs the exact path inside it */
@@ -1672,9 +1710,10 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
     return (int) hipGetLastError();
   }
   const bool late = late_issue(b->mode);
-  if (b->mode == RHP_MODE_HTTP) return launch_dfa<16, true, true>(prm, s, dev, cus);
-  if (late) return launch_dfa<16, true, false>(prm, s, dev, cus);
-  return launch_dfa<16, false, false>(prm, s, dev, cus);
+  if (b->mode == RHP_MODE_HTTP) return launch_dfa<16, true, true, false>(prm, s, dev, cus);
+  if (compact) return late ? launch_dfa<16, true, false, true>(prm, s, dev, cus) : launch_dfa<16, false, false, true>(prm, s, dev, cus);
+  if (late) return launch_dfa<16, true, false, false>(prm, s, dev, cus);
+  return launch_dfa<16, false, false, false>(prm, s, dev, cus);
 }
 
 int rhp_fixup_sessions(const rhp_batch_t *b, const rhp_session_t *sessions, uint32_t n_sessions,
@@ -1700,6 +1739,9 @@ int rhp_fixup_sessions(const rhp_batch_t *b, const rhp_session_t *sessions, uint
   const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR;
   prm.hs_req = hmajor ? 1u : b->max_headers;
   prm.hs_hdr = hmajor ? b->n : 1u;
+  prm.lens = nullptr;
+  prm.rec_req = prm.hs_req;
+  prm.rec_hdr = prm.hs_hdr;
   const uint32_t grid = (n_sessions + 255u) / 256u;
   hipLaunchKernelGGL(rhp_fixup_kernel, dim3(grid), dim3(256), 0, s, prm, sessions, n_sessions, results, req_start);
   return (int) hipGetLastError();

@@ -92,6 +92,9 @@ def test_dfa_emulation_fuzz_vs_oracle(seed, maxh):
         res, stats = rhp.emulate(buf, off, maxh, mode)
         want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
         assert_same(canon(res, mode), want, buf, off, f"emu cfg{cfg} seed{seed} maxh{maxh}")
+        if mode == rhp.MODE_PHR:   # compact records: the running sum of rhp.h gives the same offsets
+            res, _ = rhp.emulate(buf, off, maxh, mode, rhp.LAYOUT_COMPACT)
+            assert_same(canon(res, mode), want, buf, off, f"emu compact seed{seed} maxh{maxh}")
 
 
 @pytest.mark.parametrize("shift", [0, 1, 2, 3])

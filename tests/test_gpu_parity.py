@@ -30,10 +30,16 @@ def golden(name):
 @pytest.mark.parametrize("impl,layout", [(rhp.IMPL_DFA, rhp.LAYOUT_REQUEST_MAJOR), (rhp.IMPL_EXACT, rhp.LAYOUT_REQUEST_MAJOR),
                                          (rhp.IMPL_DFA, rhp.LAYOUT_HEADER_MAJOR), (rhp.IMPL_EXACT, rhp.LAYOUT_HEADER_MAJOR),
                                          (rhp.IMPL_DFA_LATE, rhp.LAYOUT_REQUEST_MAJOR),
-                                         (rhp.IMPL_DFA_LATE, rhp.LAYOUT_HEADER_MAJOR)])
+                                         (rhp.IMPL_DFA_LATE, rhp.LAYOUT_HEADER_MAJOR),
+                                         (rhp.IMPL_DFA, rhp.LAYOUT_COMPACT), (rhp.IMPL_EXACT, rhp.LAYOUT_COMPACT),
+                                         (rhp.IMPL_DFA_LATE, rhp.LAYOUT_COMPACT)])
 @pytest.mark.parametrize("name", sorted(MANIFEST))
 def test_gpu_matches_reference_golden(name, impl, layout):
     spec, buf, off, want, z = golden(name)
+    if layout == rhp.LAYOUT_COMPACT and spec["mode"] != rhp.MODE_PHR:
+        with pytest.raises(RuntimeError):   # the compact records are a phr-mode layout (rhp.h): -22
+            rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], impl=impl, layout=layout)
+        return
     res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], impl=impl, layout=layout)
     assert_same(canon(res, spec["mode"]), want, buf, off, f"GPU impl{impl} vs golden {name}")
     if "bytes_out_sha256" in z.files:
@@ -49,6 +55,32 @@ def test_gpu_reference_http_vectors():
         result, consumed = int(res.http["result"][0]), int(res.http["consumed"][0])
         remaining = len(s) - consumed if result == 1 else len(s)
         assert (result, remaining) == (v["result"], v["remaining"]), v
+
+
+@pytest.mark.parametrize("maxh", [0, 1, 3, 16, 32, 64])
+def test_gpu_compact_fuzz_vs_oracle(maxh):
+    """Compact records (RHP_LAYOUT_COMPACT): lengths from the DFA, wide records
+    from the exact path (RHP_F_WIDE) exactly where the emulator takes it; the
+    expanded records equal the oracle's."""
+    for impl, seed in ((rhp.IMPL_DFA, 9300 + maxh), (rhp.IMPL_DFA_LATE, 9400 + maxh)):
+        buf, off = rhp.generate(rhp.GEN_FUZZ, 60000, seed)
+        res = rhp.parse_batch(buf, off, maxh, rhp.MODE_PHR, impl=impl, layout=rhp.LAYOUT_COMPACT)
+        want = to_rhp(*run_oracle(buf, off, maxh, rhp.MODE_PHR)[:3], rhp.MODE_PHR)
+        assert_same(canon(res, rhp.MODE_PHR), want, buf, off, f"GPU compact fuzz impl{impl} maxh{maxh}")
+        emu, _ = rhp.emulate(buf, off, maxh, rhp.MODE_PHR, rhp.LAYOUT_COMPACT)
+        assert np.array_equal(res.reqs["flags"] & (rhp.F_EXACT | rhp.F_WIDE), emu.reqs["flags"] & (rhp.F_EXACT | rhp.F_WIDE))
+
+
+@pytest.mark.parametrize("name", ["config2_get256_h16", "config3_zipf_h32", "config4_get256_shard5of8"])
+def test_gpu_compact_full_size_matches_reference_digest(name):
+    spec = FULL[name]
+    buf, off = inputs(spec)
+    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], layout=rhp.LAYOUT_COMPACT)
+    got = canon(res, spec["mode"])
+    if record_digest(*got) != spec["records_sha256"]:
+        want = to_rhp(*run_oracle(buf, off, spec["max_headers"], spec["mode"])[:3], spec["mode"])
+        assert_same(got, want, buf, off, name)
+        raise AssertionError(f"{name}: compact digest differs from the reference but matches the oracle")
 
 
 @pytest.mark.parametrize("maxh", [0, 1, 3, 16, 32, 64])

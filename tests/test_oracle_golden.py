@@ -35,10 +35,14 @@ def test_oracle_matches_reference_golden(name):
         assert hashlib.sha256(out.tobytes()).digest() == z["bytes_out_sha256"].tobytes()
 
 
-@pytest.mark.parametrize("layout", [rhp.LAYOUT_REQUEST_MAJOR, rhp.LAYOUT_HEADER_MAJOR])
+@pytest.mark.parametrize("layout", [rhp.LAYOUT_REQUEST_MAJOR, rhp.LAYOUT_HEADER_MAJOR, rhp.LAYOUT_COMPACT])
 @pytest.mark.parametrize("name", sorted(SETS))
 def test_dfa_emulation_matches_golden(name, layout):
     spec, buf, off, want, z = load_golden(name)
+    if layout == rhp.LAYOUT_COMPACT and spec["mode"] != rhp.MODE_PHR:
+        with pytest.raises(RuntimeError):   # compact records: phr mode only (rhp.h)
+            rhp.emulate(buf, off, spec["max_headers"], spec["mode"], layout)
+        return
     res, stats = rhp.emulate(buf, off, spec["max_headers"], spec["mode"], layout)
     assert_same(canon(res, spec["mode"]), want, buf, off, f"DFA emulation vs golden {name}")
     if "bytes_out_sha256" in z.files:
@@ -50,6 +54,10 @@ def test_cpu_exact_parser_matches_golden(name):
     spec, buf, off, want, z = load_golden(name)
     res = rhp.parse_cpu_exact(buf, off, spec["max_headers"], spec["mode"], rhp.LAYOUT_HEADER_MAJOR)
     assert_same(canon(res, spec["mode"]), want, buf, off, f"CPU exact parser vs golden {name}")
+    if spec["mode"] == rhp.MODE_PHR:   # compact layout: every record wide (RHP_F_WIDE), expanded the same
+        res = rhp.parse_cpu_exact(buf, off, spec["max_headers"], spec["mode"], rhp.LAYOUT_COMPACT)
+        assert_same(canon(res, spec["mode"]), want, buf, off, f"CPU exact parser (compact) vs golden {name}")
+        assert ((res.reqs["flags"] & rhp.F_WIDE) != 0).all()
 
 
 def vectors():

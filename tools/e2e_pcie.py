@@ -3,11 +3,20 @@ ends in host memory -- the io_uring recv buffer").
 
 The batch (config 2 by default: 1M x 256 B) sits in pinned host memory; it is cut
 into chunks that stream through S HIP streams: pinned hipMemcpyAsync H2D of the
-chunk's bytes and offsets -> rhp_parse_batch on that chunk -> D2H of its request
-records and header records.  Copies of one chunk overlap the kernel of another
-and the two copy directions overlap each other.  Reports GiB/s of algorithmic
-bytes over the wall time of the whole batch, next to the device-resident kernel
-rate of the same batch and the copy-only rates.
+chunk's bytes and offsets -> rhp_parse_batch on that chunk (header-major records
+within the chunk) -> D2H of the chunk's request records.  The host reads each
+chunk's request records as they land (a consumer needs them first anyway), takes
+the largest num_headers of the chunk, and copies back only header rows
+0 .. that - 1 on a copy stream of their own -- the records the requests use, not
+every one of the max_headers slots (config 2: 16 + 4 x 8 = 48 B per request, not
+16 + 16 x 8).  Copies of one chunk overlap the kernel of another and the two
+copy directions overlap each other.
+
+Reports GiB/s of algorithmic bytes over the wall time of the whole batch, next to
+the device-resident kernel rate of the same chunks and the copy-only rates, and
+the timeline of the fastest end-to-end repetition from HIP events: per copy
+direction and for the kernels, the union of their busy intervals, so a slow run
+says which engine was busy (or idle) for how long.
 
 usage: python tools/e2e_pcie.py [--config get256] [--chunks 16] [--streams 3] [--reps 5]
 """
@@ -27,6 +36,17 @@ import libreactorng_amd as rhp  # noqa: E402
 from bench import CONFIGS  # noqa: E402
 
 
+def _union_ms(spans):
+    """total length of the union of [a, b) intervals (ms)"""
+    tot, end = 0.0, -1e30
+    for a, b in sorted(spans):
+        if b <= end:
+            continue
+        tot += b - max(a, end)
+        end = b
+    return tot
+
+
 def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
     """The end-to-end measurement as a dict (bench.py's `e2e` object)."""
     args = argparse.Namespace(config=config, n=n, chunks=chunks, streams=streams, reps=reps)
@@ -35,12 +55,16 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
     buf, off = rhp.generate(cfg["gen"], n, cfg["seed"])
     alg = rhp.header_bytes(cfg["gen"], n, cfg["seed"])
     dev = torch.device("cuda")
+    RS, HB = rhp.REQ_DTYPE.itemsize, rhp.HDR_DTYPE.itemsize
+    bounds = [n * k // args.chunks for k in range(args.chunks + 1)]
 
-    # pinned host buffers (the recv side) and full-size device mirrors
+    # pinned host buffers (the recv side) and full-size device mirrors; chunk k's
+    # header records are header-major within the chunk: row r of it is one
+    # contiguous run of (hi - lo) records at hdr_base(k) + r * (hi - lo) * 8
     h_bytes = torch.from_numpy(buf).pin_memory()
     h_off = torch.from_numpy(off.view(np.int64)).pin_memory()
-    h_reqs = torch.empty(n * rhp.REQ_DTYPE.itemsize, dtype=torch.uint8).pin_memory()
-    h_hdrs = torch.empty(n * maxh * rhp.HDR_DTYPE.itemsize, dtype=torch.uint8).pin_memory()
+    h_reqs = torch.empty(n * RS, dtype=torch.uint8).pin_memory()
+    h_hdrs = torch.zeros(n * maxh * HB, dtype=torch.uint8).pin_memory()
     d_bytes = torch.empty_like(h_bytes, device=dev)
     d_off = torch.empty_like(h_off, device=dev)
     d_reqs = torch.empty_like(h_reqs, device=dev)
@@ -48,60 +72,116 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
     d_http = torch.zeros(max(1, n if mode == rhp.MODE_HTTP else 1) * rhp.HTTP_DTYPE.itemsize,
                          dtype=torch.uint8, device=dev)
     streams = [torch.cuda.Stream() for _ in range(args.streams)]
+    rows_stream = torch.cuda.Stream()   # D2H of header rows, issued as each chunk's request records land
     works = [torch.zeros(rhp.RHP_WORK_WORDS, dtype=torch.int32, device=dev) for _ in streams]
     lib = rhp.lib()
-    bounds = [n * k // args.chunks for k in range(args.chunks + 1)]
-    RS, HS = rhp.REQ_DTYPE.itemsize, maxh * rhp.HDR_DTYPE.itemsize
+    reqs_view = h_reqs.numpy().view(rhp.REQ_DTYPE)
+    EV = lambda: torch.cuda.Event(enable_timing=True)   # noqa: E731
 
-    def run(do_h2d=True, do_kernel=True, do_d2h=True):
+    def run(do_h2d=True, do_kernel=True, do_d2h=True, timeline=None):
+        t0 = EV()
+        t0.record(streams[0])
+        for s in streams[1:] + [rows_stream]:
+            s.wait_event(t0)
+        marks = []   # per chunk: (h2d start, h2d end, kernel end, reqs end) events
         for k in range(args.chunks):
             lo, hi = bounds[k], bounds[k + 1]
             s = streams[k % len(streams)]
-            b0, b1 = int(off[lo]), int(off[hi]) + rhp.RHP_PAD   # the chunk's bytes + the pad the ABI reads
-            b1 = min(b1, buf.size)
+            b0, b1 = int(off[lo]), min(int(off[hi]) + rhp.RHP_PAD, buf.size)   # + the pad the ABI reads
+            e = [EV() for _ in range(4)]
             with torch.cuda.stream(s):
+                e[0].record(s)
                 if do_h2d:
                     d_bytes[b0:b1].copy_(h_bytes[b0:b1], non_blocking=True)
                     d_off[lo:hi + 1].copy_(h_off[lo:hi + 1], non_blocking=True)
+                e[1].record(s)
                 if do_kernel:
                     b = rhp.Batch(d_bytes.data_ptr(), d_bytes.data_ptr(), d_off.data_ptr() + 8 * lo, d_bytes.numel(),
-                                  hi - lo, maxh, mode, 0, d_reqs.data_ptr() + RS * lo, d_hdrs.data_ptr() + HS * lo,
+                                  hi - lo, maxh, mode, rhp.LAYOUT_HEADER_MAJOR, d_reqs.data_ptr() + RS * lo,
+                                  d_hdrs.data_ptr() + HB * maxh * lo,
                                   d_http.data_ptr() + (rhp.HTTP_DTYPE.itemsize * lo if mode == rhp.MODE_HTTP else 0),
                                   works[k % len(streams)].data_ptr())
                     rc = lib.rhp_parse_batch(ctypes.byref(b), ctypes.c_void_p(s.cuda_stream))
                     assert rc == 0, rc
+                e[2].record(s)
                 if do_d2h:
                     h_reqs[RS * lo:RS * hi].copy_(d_reqs[RS * lo:RS * hi], non_blocking=True)
-                    h_hdrs[HS * lo:HS * hi].copy_(d_hdrs[HS * lo:HS * hi], non_blocking=True)
+                e[3].record(s)
+            marks.append(e)
+        rows_marks, d2h_bytes = [], RS * n if do_d2h else 0
+        for k in range(args.chunks):
+            lo, hi = bounds[k], bounds[k + 1]
+            if not do_d2h:
+                continue
+            marks[k][3].synchronize()   # chunk k's request records are on the host
+            r = reqs_view[lo:hi]
+            used = int(r["num_headers"][r["ret"] > 0].max(initial=0))
+            nb = used * (hi - lo) * HB
+            base = HB * maxh * lo
+            e = [EV(), EV()]
+            with torch.cuda.stream(rows_stream):
+                e[0].record(rows_stream)
+                if nb:
+                    h_hdrs[base:base + nb].copy_(d_hdrs[base:base + nb], non_blocking=True)
+                e[1].record(rows_stream)
+            rows_marks.append(e)
+            d2h_bytes += nb
         torch.cuda.synchronize()
+        if timeline is not None:
+            ms = lambda ev: t0.elapsed_time(ev)   # noqa: E731
+            timeline.update(
+                h2d=[(ms(e[0]), ms(e[1])) for e in marks], kernel=[(ms(e[1]), ms(e[2])) for e in marks],
+                d2h_reqs=[(ms(e[2]), ms(e[3])) for e in marks], d2h_rows=[(ms(e[0]), ms(e[1])) for e in rows_marks])
+        return d2h_bytes
 
     def timed(**kw):
         run(**kw)
-        t = []
+        best, best_tl, nbytes = None, None, 0
         for _ in range(args.reps):
+            tl = {}
             t0 = time.perf_counter()
-            run(**kw)
-            t.append(time.perf_counter() - t0)
-        return min(t)
+            nbytes = run(timeline=tl, **kw)
+            t = time.perf_counter() - t0
+            if best is None or t < best:
+                best, best_tl = t, tl
+        return best, best_tl, nbytes
 
-    t_e2e = timed()
-    # parity of what came back to the host: the template answer for config 2
-    reqs = h_reqs.numpy().view(rhp.REQ_DTYPE)
+    t_e2e, tl, d2h_bytes = timed()
+    reqs = reqs_view
     ok_frac = float((reqs["ret"] > 0).mean())
-    t_h2d = timed(do_kernel=False, do_d2h=False)
-    t_d2h = timed(do_h2d=False, do_kernel=False)
-    t_kern = timed(do_h2d=False, do_d2h=False)
+    # what came back to the host, against the reference's digest of the same workload
+    from bench import golden_spec
+    spec = golden_spec(args.config, 0, n)
+    parity = "unpinned: no reference digest for this size"
+    if spec is not None:
+        hv = np.zeros((n, maxh), dtype=rhp.HDR_DTYPE)
+        flat = h_hdrs.numpy().view(rhp.HDR_DTYPE)
+        for k in range(args.chunks):
+            lo, hi = bounds[k], bounds[k + 1]
+            hv[lo:hi] = flat[maxh * lo:maxh * hi].reshape(maxh, hi - lo).T
+        res = rhp.Result(reqs.copy(), hv, None)
+        parity = "match" if rhp.record_digest(*rhp.canonical(res, mode)) == spec["records_sha256"] else \
+            "MISMATCH: the records copied back differ from the reference digest"
+    t_h2d, _, _ = timed(do_kernel=False, do_d2h=False)
+    t_kern, _, _ = timed(do_h2d=False, do_d2h=False)
     in_bytes = buf.size + off.nbytes
-    out_bytes = h_reqs.numel() + h_hdrs.numel()
     gib = 2 ** 30
+    busy = {k: round(_union_ms(v), 3) for k, v in tl.items()}
+    span = max(b for v in tl.values() for _, b in v) if tl else 0.0
     return ({
         "config": args.config, "requests": n, "algorithmic_bytes": int(alg), "chunks": args.chunks,
-        "streams": args.streams, "ok_fraction": ok_frac,
+        "streams": args.streams, "ok_fraction": ok_frac, "record_layout": "header-major per chunk",
+        "parity": parity,
         "e2e_GiBps": round(alg / t_e2e / gib, 2), "e2e_ms": round(t_e2e * 1e3, 3),
         "kernels_only_GiBps": round(alg / t_kern / gib, 2), "kernels_only_ms": round(t_kern * 1e3, 3),
         "h2d_GBps": round(in_bytes / t_h2d / 1e9, 2), "h2d_ms": round(t_h2d * 1e3, 3),
-        "d2h_GBps": round(out_bytes / t_d2h / 1e9, 2), "d2h_ms": round(t_d2h * 1e3, 3),
-        "h2d_bytes": int(in_bytes), "d2h_bytes": int(out_bytes),
+        "h2d_bytes": int(in_bytes), "d2h_bytes": int(d2h_bytes),
+        "d2h_bytes_per_request": round(d2h_bytes / n, 2),
+        # the fastest e2e repetition from HIP events: busy time (union of intervals) per engine, and the span
+        "timeline_busy_ms": busy, "timeline_span_ms": round(span, 3),
+        "timeline_note": "h2d = bytes + offsets per chunk, kernel = rhp_parse_batch per chunk, d2h_reqs = request "
+                         "records, d2h_rows = the header rows the chunk's requests use (issued when its request "
+                         "records have landed)",
     })
 
 

@@ -447,6 +447,14 @@ def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
     wall, kern_ms = runner.timed(steps)
     if dist is not None:
         dist.barrier()
+    piped = None
+    if args.pipeline_streams > 1 and args.device == "gpu" and not cfg.get("rewrites"):
+        pr = GpuRunner(cfg, lo, hi, max(args.copies, args.pipeline_streams), layout, streams=args.pipeline_streams)
+        pr.timed_pipelined(warmup)
+        pw = pr.timed_pipelined(steps)
+        piped = {"streams": args.pipeline_streams, "ms_per_step": round(pw * 1e3 / steps, 4),
+                 "value": round(float(alg_bytes) * steps / pw / 2 ** 30, 2)}
+        del pr
     # outside the timed region: the last timed launch's records against the reference's digest
     spec = golden_spec(key, lo, hi - lo)
     parity = runner.parity(spec)
@@ -473,7 +481,8 @@ def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
             parity_entry["result"] = "match on the ranks with a reference digest" if any(int(c) == 0 for c in codes) \
                 else parity_entry["result"]
     return dict(cfg=cfg, lo=lo, hi=hi, n_total=n_total, alg_bytes=alg_bytes, total_alg=total_alg, wall=wall,
-                kern_ms=kern_ms, ok_frac=ok_frac, steps=steps, warmup=warmup, parity=parity_entry, layout=lay_name)
+                kern_ms=kern_ms, ok_frac=ok_frac, steps=steps, warmup=warmup, parity=parity_entry, layout=lay_name,
+                pipelined=piped)
 
 
 def roofline(r, key):
@@ -499,6 +508,9 @@ def main(argv=None):
     ap.add_argument("--per-gpu", type=int, default=0, help="requests per GPU (default: the config's 1M)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end leg")
+    ap.add_argument("--pipeline-streams", type=int, default=0,
+                    help="also time the config's batches alternating over this many HIP streams (two or more "
+                         "batches in flight, as the reactor's slots), reported beside the single-stream value")
     ap.add_argument("--impl", type=int, default=rhp.IMPL_DFA)
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--layout", default="auto", choices=["auto"] + sorted(LAYOUTS),
@@ -566,6 +578,8 @@ def main(argv=None):
         line["parity"].update({k: v["parity"]["result"] for k, v in extra.items()})
         line["parity_detail"] = {args.config: r["parity"], **{k: v["parity"] for k, v in extra.items()}}
         line["library_sha256"] = rhp.library_sha256() if args.device == "gpu" else None
+        if r.get("pipelined"):
+            line["pipelined"] = r["pipelined"]
         if extra:
             line["extra_configs"] = extra
         if world == 1 and args.device == "gpu" and not args.no_e2e:

@@ -67,6 +67,7 @@ struct Params {
    * area at hdrs */
   uint32_t *lens;
   uint32_t rec_req, rec_hdr;
+  bool wt_records;   /* records header-major or compact in phr mode: write-through where a range is even */
 };
 
 #ifndef RHP_WAVES_PER_SIMD
@@ -552,67 +553,66 @@ __device__ __forceinline__ uint32_t lds_u8(uint32_t a)
 /* keep the compiler from sinking the computation of x into a branch */
 __device__ __forceinline__ void opaque(uint32_t &x) { asm("" : "+v"(x)); }
 
-/* The loop's record stores are write-through (sc1): the line goes to memory
- * and leaves L2, so a launch ends with no dirty record lines for the kernel
- * boundary's L2 write-back to drain (MI355X_MICROARCH.md, store flavours and
- * the boundary row).  Measured on config 2's shape (tools/ubench_ceiling.hip,
- * profiles/r04/a/ceil_r4a.txt): read + 48 B of records per request 53.9 us
- * with plain stores, 52.1 us write-through. */
+/* Write-through record stores.  With `wt` (a wave-uniform flag) the loop's
+ * record stores carry sc1: the line goes to memory and leaves L2, so a launch
+ * ends with no dirty record lines for the kernel boundary's L2 write-back to
+ * drain (MI355X_MICROARCH.md, store flavours and the boundary row).  That pays
+ * where a wave's records are whole lines -- header-major or compact records of
+ * a range whose requests are even (config 2: 70.2 -> 67.1 us, the ceiling
+ * ubench 53.9 -> 52.1 us, profiles/r04/) -- and costs where they are not:
+ * request-major records, or an uneven range's (config 3 +12 %), whose partial
+ * lines plain stores merge in L2 first; http records gained nothing (+2 %).
+ * The host enables it per launch (Params::wt_records), the kernel per range. */
+#define RHP_STORE_LANES(INSN, mask, dst, v, wt)                                                   \
+  do {                                                                                            \
+    uint64_t saved_;                                                                              \
+    if (wt)                                                                                       \
+      asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 exec, %1\n\t" INSN " %2, %3, off sc1\n\t"     \
+                   "s_mov_b64 exec, %0\n\ts_nop 1"                                              \
+                   : "=&s"(saved_) : "s"(mask), "v"(dst), "v"(v) : "memory");                    \
+    else                                                                                          \
+      asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 exec, %1\n\t" INSN " %2, %3, off\n\t"         \
+                   "s_mov_b64 exec, %0\n\ts_nop 1"                                              \
+                   : "=&s"(saved_) : "s"(mask), "v"(dst), "v"(v) : "memory");                    \
+  } while (0)
 
 /* one header record (8 B) for the lanes in `mask` (a ballot), as straight-line
  * code: exec is restored before the asm ends; the trailing s_nop covers the
  * store-data read hazard */
-__device__ __forceinline__ void store_rec_lanes(uint64_t mask, rhp_hdr_t *dst, u32x2 v)
+__device__ __forceinline__ void store_rec_lanes(uint64_t mask, rhp_hdr_t *dst, u32x2 v, bool wt)
 {
-  uint64_t saved;
-  asm volatile("s_mov_b64 %0, exec\n\t"
-               "s_mov_b64 exec, %1\n\t"
-               "global_store_dwordx2 %2, %3, off sc1\n\t"
-               "s_mov_b64 exec, %0\n\t"
-               "s_nop 1"
-               : "=&s"(saved)
-               : "s"(mask), "v"(dst), "v"(v)
-               : "memory");
+  RHP_STORE_LANES("global_store_dwordx2", mask, dst, v, wt);
 }
 /* the same for a compact header record (RHP_LAYOUT_COMPACT: name_len |
  * value_len << 16) */
-__device__ __forceinline__ void store_len_lanes(uint64_t mask, uint32_t *dst, uint32_t v)
+__device__ __forceinline__ void store_len_lanes(uint64_t mask, uint32_t *dst, uint32_t v, bool wt)
 {
-  uint64_t saved;
-  asm volatile("s_mov_b64 %0, exec\n\t"
-               "s_mov_b64 exec, %1\n\t"
-               "global_store_dword %2, %3, off sc1\n\t"
-               "s_mov_b64 exec, %0\n\t"
-               "s_nop 1"
-               : "=&s"(saved)
-               : "s"(mask), "v"(dst), "v"(v)
-               : "memory");
+  RHP_STORE_LANES("global_store_dword", mask, dst, v, wt);
 }
-/* 16 / 8 bytes, write-through, for the active lanes */
-__device__ __forceinline__ void store16_wt(void *dst, u32x4 v)
+/* the request record (16 B) for the active lanes */
+__device__ __forceinline__ void store_req(rhp_req_t *dst, u32x4 v, bool wt)
 {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
-}
-__device__ __forceinline__ void store8_wt(void *dst, u32x2 v)
-{
-  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
+  if (wt) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
+  else *GLOBAL(u32x4, dst) = v;
 }
 __device__ __forceinline__ void store_http(rhp_http_t *dst, const rhp_http_t &x)
 {
-  u32x2 v[3];
+  typedef uint32_t u32x2a8 __attribute__((ext_vector_type(2), aligned(8)));
+  u32x2a8 v[3];
   __builtin_memcpy(v, &x, sizeof x);
-  uint8_t *q = reinterpret_cast<uint8_t *>(dst);
-  store8_wt(q, v[0]);
-  store8_wt(q + 8, v[1]);
-  store8_wt(q + 16, v[2]);
+  __attribute__((address_space(1))) u32x2a8 *q = GLOBAL(u32x2a8, dst);
+  q[0] = v[0];
+  q[1] = v[1];
+  q[2] = v[2];
 }
 __device__ __forceinline__ void store_http_bad(rhp_http_t *dst)
 {
   /* {result -1, body_kind 0, consumed 0, body_len 0} */
-  uint8_t *q = reinterpret_cast<uint8_t *>(dst);
-  store8_wt(q, u32x2{0xffffffffu, 0u});
-  store8_wt(q + 8, u32x2{0u, 0u});
-  store8_wt(q + 16, u32x2{0u, 0u});
+  typedef uint32_t u32x2a8 __attribute__((ext_vector_type(2), aligned(8)));
+  __attribute__((address_space(1))) u32x2a8 *q = GLOBAL(u32x2a8, dst);
+  q[0] = u32x2a8{0xffffffffu, 0u};
+  q[1] = u32x2a8{0u, 0u};
+  q[2] = u32x2a8{0u, 0u};
 }
 
 }  // namespace
@@ -837,6 +837,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * window from dcur and nh, not carried across the walk; the host keeps
    * n * max_headers below 2^32) */
   uint32_t hx = 0;
+  bool wt = false;   /* write-through record stores (set once the range is known even, below) */
   auto word = [&](uint32_t m, uint32_t base) {
     m &= dstop - 1u;   /* nothing after a max_headers stop */
     if (!__builtin_amdgcn_ballot_w64(m != 0)) return;
@@ -873,8 +874,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         const uint32_t e = base + (uint32_t) __builtin_ctz(eolm | 0x80000000u);
         const uint32_t co = t ? pco : base + (uint32_t) __builtin_ctz(com | 0x80000000u);
         const uint32_t lo = ls | ((co - ls) << 16), hi = (co + 2u) | ((e - co - 3u) << 16);
-        if constexpr (COMPACT) store_len_lanes(st_m, p.lens + hx, (co - ls) | ((e - co - 3u) << 16));
-        else store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi});
+        if constexpr (COMPACT) store_len_lanes(st_m, p.lens + hx, (co - ls) | ((e - co - 3u) << 16), wt);
+        else store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi}, wt);
         if (http) {   /* uniform: framing candidates only in http mode */
           const uint32_t nlen = co - ls;
           const bool cnd = has && (nlen == 14u || nlen == 17u);
@@ -907,8 +908,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const uint32_t lo = ls | ((co - ls) << 16), hi = (co + 2u) | ((e - co - 3u) << 16);
       const uint64_t st_m = __builtin_amdgcn_ballot_w64(rec);
       if (st_m) {
-        if constexpr (COMPACT) store_len_lanes(st_m, p.lens + hx, (co - ls) | ((e - co - 3u) << 16));
-        else store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi});
+        if constexpr (COMPACT) store_len_lanes(st_m, p.lens + hx, (co - ls) | ((e - co - 3u) << 16), wt);
+        else store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi}, wt);
       }
       if (http) {
         const uint32_t nlen = co - ls;
@@ -1140,7 +1141,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         }
         if (!framed) {
           defer(dcur);
-          store16_wt(&p.http[dcur], u32x4{cand, kHintFrame | (term_pos + 1u), crec_lo, crec_hi});
+          typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+          *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{cand, kHintFrame | (term_pos + 1u), crec_lo, crec_hi};
         }
       }
     } else if (bad) {
@@ -1149,9 +1151,12 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     } else {
       rq[3] = (uint32_t) kDeferExact << 16;   /* exact path: replay */
       defer(dcur);
-      if (http) store16_wt(&p.http[dcur], u32x4{0u, kHintExact, 0u, 0u});
+      if (http) {
+        typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+        *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{0u, kHintExact, 0u, 0u};
+      }
     }
-    store16_wt(p.reqs + dcur, rq);
+    store_req(p.reqs + dcur, rq, wt);
     dhas = false;
     return true;
   };
@@ -1256,6 +1261,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   dg.loads_landed();
   const bool uneven =
       may_order && __builtin_amdgcn_ballot_w64((uint64_t) (s1 - s0) * span_n > 2u * (o_hi - o_lo)) != 0;
+  wt = p.wt_records && !uneven;
   /* An uneven range runs on 12 of the 16 waves: its end is set by its longest
    * requests (each walked by one lane from the first iteration on), and with
    * fewer waves sharing the CU every iteration is shorter while the lanes'
@@ -1308,8 +1314,23 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #ifndef RHP_PRIO_PHASE_SHIFT
 #define RHP_PRIO_PHASE_SHIFT 6
 #endif
+#ifndef RHP_PRIO_MODE
+#define RHP_PRIO_MODE 0
+#endif
   uint32_t prio_it = (tid >> RHP_PRIO_PHASE_SHIFT) & 3u;
+#if RHP_PRIO_MODE == 1
+  /* static, graded by dispatch order: the younger a wave on its SIMD, the higher */
+  switch ((tid >> 8) & 3u) {
+  case 0: __builtin_amdgcn_s_setprio(0); break;
+  case 1: __builtin_amdgcn_s_setprio(1); break;
+  case 2: __builtin_amdgcn_s_setprio(2); break;
+  default: __builtin_amdgcn_s_setprio(3);
+  }
+#elif RHP_PRIO_MODE == 2
+  if ((tid >> 9) & 1u) __builtin_amdgcn_s_setprio(1);   /* static: the younger half of the workgroup */
+#endif
   while (!idle_wave) {
+#if RHP_PRIO_MODE == 0
     prio_it = (prio_it + 1u) & 3u;
     switch (prio_it) {
     case 0: __builtin_amdgcn_s_setprio(0); break;
@@ -1317,6 +1338,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     case 2: __builtin_amdgcn_s_setprio(2); break;
     default: __builtin_amdgcn_s_setprio(3);
     }
+#endif
     dg.mark();
     /* [A] */
     wait_vm0();   /* the window's LDS-DMA has landed (and the pending offsets, and older stores) */
@@ -1694,6 +1716,7 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.lens = nullptr;
   prm.rec_req = prm.hs_req;
   prm.rec_hdr = prm.hs_hdr;
+  prm.wt_records = b->mode == RHP_MODE_PHR && b->layout != RHP_LAYOUT_REQUEST_MAJOR;
   if (compact) {   /* lengths header-major at hdrs, the wide records request-major behind them */
     prm.lens = reinterpret_cast<uint32_t *>(b->hdrs);
     prm.hdrs = reinterpret_cast<rhp_hdr_t *>(reinterpret_cast<uint8_t *>(b->hdrs) + RHP_COMPACT_WIDE_OFF(b->n, b->max_headers));
@@ -1742,6 +1765,7 @@ int rhp_fixup_sessions(const rhp_batch_t *b, const rhp_session_t *sessions, uint
   prm.lens = nullptr;
   prm.rec_req = prm.hs_req;
   prm.rec_hdr = prm.hs_hdr;
+  prm.wt_records = false;
   const uint32_t grid = (n_sessions + 255u) / 256u;
   hipLaunchKernelGGL(rhp_fixup_kernel, dim3(grid), dim3(256), 0, s, prm, sessions, n_sessions, results, req_start);
   return (int) hipGetLastError();

@@ -55,7 +55,7 @@ METRIC = "GiB/s device-resident batched HTTP/1.1 request parse, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E, GB/s (MI355X_MICROARCH.md chip table)
 CONFIGS = {
     "get256": dict(gen=rhp.GEN_GET256, seed=0x5EED0002, maxh=16, mode=rhp.MODE_PHR, per_gpu=1 << 20,
-                   layout="header",
+                   layout="compact",
                    name="config2/4: 1M x 256 B GET, 4 headers per GPU (phr_parse_request, max_headers 16)"),
     "zipf": dict(gen=rhp.GEN_ZIPF, seed=0x5EED0003, maxh=32, mode=rhp.MODE_PHR, per_gpu=1 << 20,
                  layout="request",
@@ -515,8 +515,8 @@ def main(argv=None):
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--layout", default="auto", choices=["auto"] + sorted(LAYOUTS),
                     help="header record layout of the batch ABI (include/rhp.h rhp_layout); auto: the "
-                         "config's (header-major for the uniform batches of configs 2/4/5, request-major "
-                         "for config 3's mixed one)")
+                         "config's (compact 4-byte records for the uniform phr batches of configs 2/4, "
+                         "header-major for config 5 (http mode), request-major for config 3's mixed one)")
     argv = sys.argv[1:] if argv is None else argv
     args = ap.parse_args(argv)
 

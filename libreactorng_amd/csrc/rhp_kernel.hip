@@ -77,7 +77,7 @@ struct Params {
 enum : uint32_t {
   kSecDecodeStamp = 6,                           /* Diag section slots of the late form's decode / framing */
   kSecFrameStamp = 7,
-  kBlock = 128,                                  /* window bytes per lane per loop iteration */
+  kBlock = 128,                                  /* window bytes per lane per loop iteration (early form) */
   kParts = kBlock / 16,                          /* 16-byte parts per window */
   kEvWords = kBlock / 32,                        /* 32-bit event words per window */
   kLdsTable = (kTable2Bytes + 1023u) & ~1023u,   /* staging starts 1 KiB aligned */
@@ -112,6 +112,14 @@ enum : uint32_t {
   kPoolBytes = 4 * kPoolWords + 2 * kDeferCap
 };
 static_assert(idx2(S_DONE, 0) == kPark, "parked lanes sit in DONE");
+
+/* http mode's window extension (16-byte parts past the 128-byte window, see
+ * the kernel's window geometry) and the waves its staging leaves room for */
+#ifndef RHP_HTTP_XPARTS
+#define RHP_HTTP_XPARTS 2
+#endif
+constexpr uint32_t kHttpXParts = RHP_HTTP_XPARTS;
+constexpr int kHttpWaves = kHttpXParts == 0 ? 16 : kHttpXParts <= 2 ? 12 : 8;
 
 /* LDS byte address of part q (16 B) of lane w's window inside the staging
  * buffer.  The LDS-DMA loads of a wave write lane-linearly (1 KiB per
@@ -638,6 +646,19 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 
   const uint32_t maxh = p.max_headers;
   constexpr bool http = HTTP;   /* p.mode == RHP_MODE_HTTP (the launch picks the instance) */
+  /* Window geometry.  The early form walks 128-byte windows (whole HBM lines);
+   * the http form's windows are kXParts 16-byte parts longer (kHttpXParts):
+   * the bytes of the next line a header section most often still needs, so
+   * a request whose header section fits (config 5: 133 B) is walked, decoded
+   * and framed in ONE iteration where 128 B took two -- the second for the
+   * few bytes up to its CRLFCRLF.  The extension parts go to a staging area of
+   * their own (xstage: part 8 + k of every lane's window at 1024 k + 16 lane),
+   * fetched by kXParts more LDS-DMA loads per issue. */
+  constexpr uint32_t kXParts = (LATE && HTTP) ? kHttpXParts : 0u;
+  constexpr uint32_t kWParts = kParts + kXParts;   /* 16-byte parts per window */
+  constexpr uint32_t kWBlock = 16u * kWParts;      /* window bytes */
+  constexpr uint32_t kWEv = kWBlock / 32u;         /* 32-bit event words per window */
+  static_assert(kWBlock % 32u == 0, "whole event words per window");
 
   /* ---- request pool ----
    * Workgroup g owns requests [g*span, (g+1)*span) (host: span = n / grid).
@@ -698,14 +719,21 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   bool wact = false;                   /* wcur is live: its walk has not ended */
   uint32_t wcur = 0, wlen = 0, wget = 0, cur_ptr = 0;
   uint32_t woff = 0;                   /* wcur's first byte, offset from base (LATE http framing) */
-  uint32_t ev[kEvWords];               /* events of the window being walked (32 bytes per word) */
+  uint32_t ev[kWEv];                   /* events of the window being walked (32 bytes per word) */
   bool pend_ok = false;                /* pend: the lane's next request */
   uint32_t pend = 0;
   uint32_t pend_o0 = 0, pend_o1 = 0;   /* low dwords of offsets[pend], offsets[pend+1] as loaded */
   uint32_t nw = 0;                     /* next window: byte offset from base | kind (0 none, 1
                                           continuation, 2 first window of pend); windows are 4-aligned */
-  u32x4 W[kParts];                     /* the window in registers */
+  u32x4 W[kWParts];                    /* the window in registers */
   const uint32_t stage = __builtin_amdgcn_readfirstlane(kLdsTable + (tid >> 6) * kStageWave);   /* wave-uniform */
+  /* the extension parts of the wave's windows (kXParts > 0): after the pool area */
+  const uint32_t xstage = __builtin_amdgcn_readfirstlane(kLdsTable + WAVES * kStageWave + kPoolBytes +
+                                                         (tid >> 6) * 1024u * kXParts);
+  /* LDS address of part q of this lane's window */
+  auto part_lds = [&](uint32_t q) -> uint32_t {
+    return q < kParts ? stage + stage_off(lane, q) : xstage + 1024u * (q - kParts) + 16u * lane;
+  };
 
   /* ---- decode state (the request whose previous window is decoded) ----
    *   kn   request-line events consumed (0 ME, 1 PE, 2 RL, 3 done) | minor << 3
@@ -720,7 +748,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   bool dhas = false;
   uint32_t dcur = 0, dlen = 0, st_prev = kPark, doff = 0;
   int32_t dpos = 0;                    /* position of the decoded window's first byte */
-  uint32_t evp[kEvWords];              /* its events */
+  uint32_t evp[kWEv];                  /* its events */
   uint32_t kn = 0, me = 0, pe = 0, rl = 0, nh = 0, ls = 0, t = 0, pco = 0, ovf = 0;
   uint32_t cand = 0, crec_lo = 0, crec_hi = 0;
   /* http framing in the late-issue kernel (http.c:196-218), from the
@@ -732,7 +760,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   uint32_t fr = 0;
   uint64_t fv = 0;
 #pragma unroll
-  for (int w = 0; w < (int) kEvWords; w++) ev[w] = evp[w] = 0;
+  for (int w = 0; w < (int) kWEv; w++) ev[w] = evp[w] = 0;
 
   /* give every lane without a pending request one from the pool; the offsets
    * loads are only consumed at the top of the next block */
@@ -831,7 +859,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * exceeds maxh and every completed record is stored.  Updates are written as
    * arithmetic on the conditions (m & (m - c), x + c * d) so the compiler emits
    * straight-line code, not exec-masked branches. */
-  uint32_t mq[kEvWords];
+  uint32_t mq[kWEv];
   uint32_t term_pos = 0xffffffffu, dstop = 0;
   /* hx: index in hdrs of the decoded request's next header record (set per
    * window from dcur and nh, not carried across the walk; the host keeps
@@ -937,7 +965,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   };
   auto decode_window = [&]() {
 #pragma unroll
-    for (int q = 0; q < (int) kEvWords; q++) word(mq[q], (uint32_t) dpos + 32u * (uint32_t) q);
+    for (int q = 0; q < (int) kWEv; q++) word(mq[q], (uint32_t) dpos + 32u * (uint32_t) q);
   };
   /* The framing candidate's evaluation after a window's decode (see fr).  A
    * lane that needs bytes reads the 36 bytes from one position r of the
@@ -946,7 +974,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * with both names) and its value from r + 16 (the one SP after the colon),
    * or the continuation of a Content-Length value from r. */
   auto frame_window = [&](uint32_t crec_before) __attribute__((always_inline)) {
-    const uint32_t wend = (uint32_t) dpos + kBlock;
+    const uint32_t wend = (uint32_t) dpos + kWBlock;
     const uint32_t hdr = cand & 0x3fffffffu;
     const bool rec_done = (crec_lo | (cand & 0xbfffffffu)) != crec_before && hdr != 0 && (hdr & (hdr - 1u)) == 0 &&
                           !(cand >> 31);
@@ -987,10 +1015,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     uint32_t raw[10], d[9];
     const uint32_t b0 = (r - (uint32_t) dpos) & ~3u, sh = (r - (uint32_t) dpos) & 3u;
 #pragma unroll
-    for (uint32_t k = 0; k < 10; k++) {   /* bytes past the window wrap inside the lane's slot: never used */
+    for (uint32_t k = 0; k < 10; k++) {   /* bytes past the window wrap inside the lane's window: never used */
       const uint32_t b = b0 + 4u * k;
       raw[k] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(
-          (size_t) (stage + stage_off(lane, (b >> 4) & 7u) + (b & 15u)));
+          (size_t) (part_lds((b >> 4) % kWParts) + (b & 15u)));
     }
 #pragma unroll
     for (uint32_t k = 0; k < 9; k++) d[k] = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh);
@@ -1060,18 +1088,24 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const bool term_ev = is_done2(e) || is_err2(e);
     const uint32_t live = (slow || !dhas || ovf) ? 0u : 0xffffffffu;
 #pragma unroll
-    for (int q = 0; q < (int) kEvWords; q++) mq[q] = evp[q] & live;
+    for (int q = 0; q < (int) kWEv; q++) mq[q] = evp[q] & live;
     term_pos = 0xffffffffu;
     dstop = 0;
     hx = dcur * p.rec_req + nh * p.rec_hdr;
     if (term_ev) {   /* the terminal is the window's last event: take it off the mask */
-      const int q = mq[3] ? 3 : mq[2] ? 2 : mq[1] ? 1 : 0;
-      uint32_t w = q == 3 ? mq[3] : q == 2 ? mq[2] : q == 1 ? mq[1] : mq[0];
+      /* the last word with an event (selects, no dynamic register index) */
+      int q = 0;
+      uint32_t w = mq[0];
+#pragma unroll
+      for (int k = 1; k < (int) kWEv; k++) {
+        q = mq[k] ? k : q;
+        w = mq[k] ? mq[k] : w;
+      }
       const uint32_t bt = 31u - (uint32_t) __builtin_clz(w | 1u);
       if (w) term_pos = (uint32_t) dpos + 32u * (uint32_t) q + bt;
       w &= ~(1u << bt);
 #pragma unroll
-      for (int k = 0; k < (int) kEvWords; k++) mq[k] = k == q ? w : mq[k];
+      for (int k = 0; k < (int) kWEv; k++) mq[k] = k == q ? w : mq[k];
     }
   };
   /*
@@ -1085,7 +1119,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const uint32_t e = st_prev;
     const bool ovfl = ovf != 0;
     const bool term_ev = is_done2(e) || is_err2(e);
-    const bool fin = dhas && (ovfl || is_slow2(e) || term_ev || (uint32_t) dpos + kBlock >= dlen);
+    const bool fin = dhas && (ovfl || is_slow2(e) || term_ev || (uint32_t) dpos + kWBlock >= dlen);
     if (!fin) return false;
     bool ok = !ovfl && is_done2(e) && term_pos < dlen && term_pos < RHP_MAX_LEN;
     /* an ERR between the path and the request-line end (the version, kn == 2)
@@ -1185,8 +1219,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     codes_a(W[0], r);
     codes_b(W[0], r, c);
 #pragma unroll
-    for (int q = 0; q < (int) kParts; q++) {
-      const bool nx = q + 1 < (int) kParts;
+    for (int q = 0; q < (int) kWParts; q++) {
+      const bool nx = q + 1 < (int) kWParts;
       uint32_t cn[8];
 #pragma unroll
       for (int j = 0; j < 8; j++) {
@@ -1235,6 +1269,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     }
     if (nt) { RHP_ISSUE_LOADS(2) } else { RHP_ISSUE_LOADS(0) }
 #undef RHP_ISSUE_LOADS
+    /* the extension parts: lane j's own window, part 8 + k at xstage + 1024 k + 16 j */
+#pragma unroll
+    for (uint32_t k = 0; k < kXParts; k++)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (__attribute__((address_space(3))) void *) (lds + xstage + 1024u * k),
+                                               16, src + kBlock + 16u * k, 0, 0, 0);
   };
 
   /* Uneven ranges (config 3) order the hand-out from the first request on;
@@ -1345,7 +1384,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     dg.section(0);
     const uint32_t p_o0 = pend_o0, p_o1 = pend_o1;
 #pragma unroll
-    for (int q = 0; q < (int) kParts; q++) W[q] = *reinterpret_cast<const u32x4 *>(lds + stage + stage_off(lane, q));
+    for (int q = 0; q < (int) kWParts; q++) W[q] = *reinterpret_cast<const u32x4 *>(lds + part_lds((uint32_t) q));
     /* [C] */
     const uint32_t nw_kind = nw & 3u;
     bool wnew = false;
@@ -1375,7 +1414,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     if constexpr (!LATE) {
       /* [E] next window: continuation of wcur, else the first window of a ready pend */
       nw = 0;
-      if (walking && (uint32_t) (wpos + (int32_t) kBlock) < wlen) nw = (cur_ptr + kBlock) | 1u;
+      if (walking && (uint32_t) (wpos + (int32_t) kWBlock) < wlen) nw = (cur_ptr + kWBlock) | 1u;
       else if (pend_ready) nw = ((p_o0 & ~3u) - (uint32_t) base) | 2u;
       wait_lgkm0();   /* [A]'s reads of the buffer are done */
       issue();
@@ -1384,7 +1423,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       decode_begin();
       if (any_dec) decode_window();
 #pragma unroll
-      for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
+      for (int w = 0; w < (int) kWEv; w++) ev[w] = 0;
       dg.section(2, true, true);
       if (any_walk) {
         if (!walking) st = kPark;   /* idle lanes step in the parked terminal state */
@@ -1401,7 +1440,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       (void) any_dec;
       dg.section(1);
 #pragma unroll
-      for (int w = 0; w < (int) kEvWords; w++) ev[w] = 0;
+      for (int w = 0; w < (int) kWEv; w++) ev[w] = 0;
       if (any_walk) {
         if (!walking) st = kPark;
         walk();
@@ -1421,7 +1460,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       dpos = wpos;
       st_prev = st;
 #pragma unroll
-      for (int w = 0; w < (int) kEvWords; w++) evp[w] = ev[w];
+      for (int w = 0; w < (int) kWEv; w++) evp[w] = ev[w];
       decode_begin();
       const uint32_t crec_before = crec_lo | (cand & 0xbfffffffu);
       if (any_walk) decode_window();
@@ -1433,11 +1472,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       /* the walk of wcur ends with this window: finalized (a terminal, a
        * max_headers stop), or its last byte */
       if (walking && (done || is_done2(st) || is_err2(st) || is_slow2(st) ||
-                      (uint32_t) (wpos + (int32_t) kBlock) >= wlen))
+                      (uint32_t) (wpos + (int32_t) kWBlock) >= wlen))
         wact = false;
       /* [E] (the decode above read the staging buffer the issue refills) */
       nw = 0;
-      if (walking && wact) nw = (cur_ptr + kBlock) | 1u;
+      if (walking && wact) nw = (cur_ptr + kWBlock) | 1u;
       else if (pend_ok) nw = ((pend_o0 & ~3u) - (uint32_t) base) | 2u;
       wait_lgkm0();
       issue();
@@ -1461,14 +1500,14 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       dpos = wpos;
       st_prev = st;
 #pragma unroll
-      for (int w = 0; w < (int) kEvWords; w++) evp[w] = ev[w];
+      for (int w = 0; w < (int) kWEv; w++) evp[w] = ev[w];
       /* the walk of wcur ends with this window: a terminal, or its last byte */
-      if (is_done2(st) || is_err2(st) || is_slow2(st) || (uint32_t) (wpos + (int32_t) kBlock) >= wlen) wact = false;
+      if (is_done2(st) || is_err2(st) || is_slow2(st) || (uint32_t) (wpos + (int32_t) kWBlock) >= wlen) wact = false;
     } else {
       dhas = false;
     }
     }
-    wpos += (int32_t) kBlock;
+    wpos += (int32_t) kWBlock;
     dg.iteration_end();
     if (!__ballot(dhas || nw || pend_ok)) break;
   }
@@ -1618,7 +1657,10 @@ int device_cus(int dev, int *cus)
 template <int WAVES, bool LATE, bool HTTP, bool COMPACT>
 int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
 {
-  const size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes;
+  constexpr uint32_t kX = (LATE && HTTP) ? kHttpXParts : 0u;
+  const size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes + (size_t) WAVES * 1024u * kX;
+  static_assert(kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes + (size_t) WAVES * 1024u * kX <= 160u * 1024u,
+                "the workgroup's LDS fits the CU's 160 KiB");
   const uint64_t bit = 1ull << (8 * (WAVES / 4) + (COMPACT ? 4 : 0) + (LATE ? 2 : 0) + (HTTP ? 1 : 0));
   if (!(g_attr[dev].load(std::memory_order_acquire) & bit)) {
     /* idempotent: two threads of one device may both set it */
@@ -1733,7 +1775,7 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
     return (int) hipGetLastError();
   }
   const bool late = late_issue(b->mode);
-  if (b->mode == RHP_MODE_HTTP) return launch_dfa<16, true, true, false>(prm, s, dev, cus);
+  if (b->mode == RHP_MODE_HTTP) return launch_dfa<kHttpWaves, true, true, false>(prm, s, dev, cus);
   if (compact) return late ? launch_dfa<16, true, false, true>(prm, s, dev, cus) : launch_dfa<16, false, false, true>(prm, s, dev, cus);
   if (late) return launch_dfa<16, true, false, false>(prm, s, dev, cus);
   return launch_dfa<16, false, false, false>(prm, s, dev, cus);

@@ -3,14 +3,16 @@ ends in host memory -- the io_uring recv buffer").
 
 The batch (config 2 by default: 1M x 256 B) sits in pinned host memory; it is cut
 into chunks that stream through S HIP streams: pinned hipMemcpyAsync H2D of the
-chunk's bytes and offsets -> rhp_parse_batch on that chunk (header-major records
-within the chunk) -> D2H of the chunk's request records.  The host reads each
-chunk's request records as they land (a consumer needs them first anyway), takes
-the largest num_headers of the chunk, and copies back only header rows
-0 .. that - 1 on a copy stream of their own -- the records the requests use, not
-every one of the max_headers slots (config 2: 16 + 4 x 8 = 48 B per request, not
-16 + 16 x 8).  Copies of one chunk overlap the kernel of another and the two
-copy directions overlap each other.
+chunk's bytes and offsets -> rhp_parse_batch on that chunk (header records
+header-major within the chunk: compact 4-byte records in phr mode, rhp.h) -> D2H
+of the chunk's request records.  The host reads each chunk's request records as
+they land (a consumer needs them first anyway), takes the largest num_headers of
+the chunk, and copies back only header rows 0 .. that - 1 on a copy stream of
+their own -- the records the requests use, not every one of the max_headers
+slots (config 2: 16 + 4 x 4 = 32 B per request, not 16 + 16 x 8), plus the
+chunk's wide records when one of its requests took the exact path.  Copies of
+one chunk overlap the kernel of another and the two copy directions overlap
+each other.
 
 Reports GiB/s of algorithmic bytes over the wall time of the whole batch, next to
 the device-resident kernel rate of the same chunks and the copy-only rates, and
@@ -55,8 +57,15 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
     buf, off = rhp.generate(cfg["gen"], n, cfg["seed"])
     alg = rhp.header_bytes(cfg["gen"], n, cfg["seed"])
     dev = torch.device("cuda")
-    RS, HB = rhp.REQ_DTYPE.itemsize, rhp.HDR_DTYPE.itemsize
+    RS = rhp.REQ_DTYPE.itemsize
     bounds = [n * k // args.chunks for k in range(args.chunks + 1)]
+    # phr mode: compact records (rhp.h RHP_LAYOUT_COMPACT: a 4-byte record per header, header-major in
+    # the chunk, the exact path's requests in the chunk's wide area); http mode: header-major rhp_hdr_t
+    layout = rhp.LAYOUT_COMPACT if mode == rhp.MODE_PHR else rhp.LAYOUT_HEADER_MAJOR
+    HB = 4 if layout == rhp.LAYOUT_COMPACT else rhp.HDR_DTYPE.itemsize   # bytes per record of a row
+    hbase = [0]
+    for k in range(args.chunks):
+        hbase.append(hbase[-1] + ((rhp.hdrs_bytes(bounds[k + 1] - bounds[k], maxh, layout) + 255) & ~255))
 
     # pinned host buffers (the recv side) and full-size device mirrors; chunk k's
     # header records are header-major within the chunk: row r of it is one
@@ -64,7 +73,7 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
     h_bytes = torch.from_numpy(buf).pin_memory()
     h_off = torch.from_numpy(off.view(np.int64)).pin_memory()
     h_reqs = torch.empty(n * RS, dtype=torch.uint8).pin_memory()
-    h_hdrs = torch.zeros(n * maxh * HB, dtype=torch.uint8).pin_memory()
+    h_hdrs = torch.zeros(hbase[-1], dtype=torch.uint8).pin_memory()
     d_bytes = torch.empty_like(h_bytes, device=dev)
     d_off = torch.empty_like(h_off, device=dev)
     d_reqs = torch.empty_like(h_reqs, device=dev)
@@ -97,8 +106,8 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
                 e[1].record(s)
                 if do_kernel:
                     b = rhp.Batch(d_bytes.data_ptr(), d_bytes.data_ptr(), d_off.data_ptr() + 8 * lo, d_bytes.numel(),
-                                  hi - lo, maxh, mode, rhp.LAYOUT_HEADER_MAJOR, d_reqs.data_ptr() + RS * lo,
-                                  d_hdrs.data_ptr() + HB * maxh * lo,
+                                  hi - lo, maxh, mode, layout, d_reqs.data_ptr() + RS * lo,
+                                  d_hdrs.data_ptr() + hbase[k],
                                   d_http.data_ptr() + (rhp.HTTP_DTYPE.itemsize * lo if mode == rhp.MODE_HTTP else 0),
                                   works[k % len(streams)].data_ptr())
                     rc = lib.rhp_parse_batch(ctypes.byref(b), ctypes.c_void_p(s.cuda_stream))
@@ -117,15 +126,21 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
             r = reqs_view[lo:hi]
             used = int(r["num_headers"][r["ret"] > 0].max(initial=0))
             nb = used * (hi - lo) * HB
-            base = HB * maxh * lo
+            base = hbase[k]
+            # compact: requests the exact path parsed keep their records in the chunk's wide area
+            wide = layout == rhp.LAYOUT_COMPACT and bool((r["flags"] & rhp.F_WIDE).any())
+            w0 = base + ((4 * (hi - lo) * maxh + 15) & ~15)
+            wn = (hi - lo) * maxh * rhp.HDR_DTYPE.itemsize if wide else 0
             e = [EV(), EV()]
             with torch.cuda.stream(rows_stream):
                 e[0].record(rows_stream)
                 if nb:
                     h_hdrs[base:base + nb].copy_(d_hdrs[base:base + nb], non_blocking=True)
+                if wn:
+                    h_hdrs[w0:w0 + wn].copy_(d_hdrs[w0:w0 + wn], non_blocking=True)
                 e[1].record(rows_stream)
             rows_marks.append(e)
-            d2h_bytes += nb
+            d2h_bytes += nb + wn
         torch.cuda.synchronize()
         if timeline is not None:
             ms = lambda ev: t0.elapsed_time(ev)   # noqa: E731
@@ -155,10 +170,10 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
     parity = "unpinned: no reference digest for this size"
     if spec is not None:
         hv = np.zeros((n, maxh), dtype=rhp.HDR_DTYPE)
-        flat = h_hdrs.numpy().view(rhp.HDR_DTYPE)
+        raw = h_hdrs.numpy()
         for k in range(args.chunks):
             lo, hi = bounds[k], bounds[k + 1]
-            hv[lo:hi] = flat[maxh * lo:maxh * hi].reshape(maxh, hi - lo).T
+            hv[lo:hi] = rhp.expand_records(reqs[lo:hi], raw[hbase[k]:hbase[k + 1]], hi - lo, maxh, layout)
         res = rhp.Result(reqs.copy(), hv, None)
         parity = "match" if rhp.record_digest(*rhp.canonical(res, mode)) == spec["records_sha256"] else \
             "MISMATCH: the records copied back differ from the reference digest"
@@ -170,7 +185,8 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
     span = max(b for v in tl.values() for _, b in v) if tl else 0.0
     return ({
         "config": args.config, "requests": n, "algorithmic_bytes": int(alg), "chunks": args.chunks,
-        "streams": args.streams, "ok_fraction": ok_frac, "record_layout": "header-major per chunk",
+        "streams": args.streams, "ok_fraction": ok_frac,
+        "record_layout": ("compact" if layout == rhp.LAYOUT_COMPACT else "header-major") + " per chunk",
         "parity": parity,
         "e2e_GiBps": round(alg / t_e2e / gib, 2), "e2e_ms": round(t_e2e * 1e3, 3),
         "kernels_only_GiBps": round(alg / t_kern / gib, 2), "kernels_only_ms": round(t_kern * 1e3, 3),

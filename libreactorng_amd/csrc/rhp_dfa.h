@@ -58,6 +58,12 @@
 #ifndef RHP_BLOCK
 #define RHP_BLOCK 64
 #endif
+/* http mode's window extension in 16-byte parts: its windows are RHP_BLOCK +
+ * 16 * RHP_HTTP_XPARTS bytes (rhp_kernel.hip, window geometry) */
+#ifndef RHP_HTTP_XPARTS
+#define RHP_HTTP_XPARTS 2
+#endif
+#define RHP_HTTP_BLOCK (RHP_BLOCK + 16 * RHP_HTTP_XPARTS)
 
 namespace rhp {
 

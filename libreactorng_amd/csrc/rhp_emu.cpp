@@ -95,39 +95,43 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
     const uint64_t hs_hdr = b->layout == RHP_LAYOUT_HEADER_MAJOR ? b->n : 1u;
     rhp_hdr_t *hout = compact ? nullptr : b->hdrs + i * hs_req;
     uint32_t *lens = compact ? reinterpret_cast<uint32_t *>(b->hdrs) + i : nullptr;   /* lens[k * n + i] */
+    /* the kernel's window: http mode walks RHP_HTTP_BLOCK bytes per window */
+    const int32_t block = b->mode == RHP_MODE_HTTP ? RHP_HTTP_BLOCK : RHP_BLOCK;
+    constexpr int kMaxWords = (RHP_HTTP_BLOCK > RHP_BLOCK ? RHP_HTTP_BLOCK : RHP_BLOCK) / 32;
+    const int words = block / 32;
     for (;;) {
-      /* one RHP_BLOCK-byte block: steps, then the decode of its event mask */
+      /* one window: steps, then the decode of its event mask (32 bytes per word) */
       const int32_t block_pos = pos;
-      uint64_t evw[RHP_BLOCK / 64];
-      for (int w = 0; w < RHP_BLOCK / 64; w++) {
-        uint64_t ev = 0;
-        for (int k = 0; k < 64; k += 2) {   /* one table read per byte pair */
-          st = T.b[st * 256u + cls[win[64 * w + k]] * 16u + cls[win[64 * w + k + 1]]];
-          ev |= (uint64_t) (st & 3u) << k;
+      uint32_t evw[kMaxWords];
+      for (int w = 0; w < words; w++) {
+        uint32_t ev = 0;
+        for (int k = 0; k < 32; k += 2) {   /* one table read per byte pair */
+          st = T.b[st * 256u + cls[win[32 * w + k]] * 16u + cls[win[32 * w + k + 1]]];
+          ev |= (st & 3u) << k;
         }
         evw[w] = ev;
       }
-      win += RHP_BLOCK;
-      pos += RHP_BLOCK;
+      win += block;
+      pos += block;
       const bool slow = is_slow2(st);
       const bool term_ev = is_done2(st) || is_err2(st);
       uint32_t term_pos = 0xffffffffu;
-      if (term_ev) {   /* the terminal is the block's last event */
-        for (int w = RHP_BLOCK / 64 - 1; w >= 0; w--)
+      if (term_ev) {   /* the terminal is the window's last event */
+        for (int w = words - 1; w >= 0; w--)
           if (evw[w]) {
-            const uint32_t bt = 63u - (uint32_t) __builtin_clzll(evw[w]);
-            term_pos = (uint32_t) (block_pos + 64 * w) + bt;
-            evw[w] &= ~(1ull << bt);
+            const uint32_t bt = 31u - (uint32_t) __builtin_clz(evw[w]);
+            term_pos = (uint32_t) (block_pos + 32 * w) + bt;
+            evw[w] &= ~(1u << bt);
             break;
           }
       }
-      for (int w = 0; w < RHP_BLOCK / 64 && !slow; w++) {
-        uint64_t m = evw[w];
+      for (int w = 0; w < words && !slow; w++) {
+        uint32_t m = evw[w];
         while (m && !d.ovf) {
-          const uint32_t bit = (uint32_t) __builtin_ctzll(m);
+          const uint32_t bit = (uint32_t) __builtin_ctz(m);
           m &= m - 1;
           uint32_t lo, hi;
-          if (dec_event(d, (uint32_t) (block_pos + 64 * w) + bit, maxh, lo, hi)) {
+          if (dec_event(d, (uint32_t) (block_pos + 32 * w) + bit, maxh, lo, hi)) {
             if (compact) {   /* as the kernel: the two lengths (rhp.h RHP_LAYOUT_COMPACT) */
               lens[(uint64_t) (d.nh - 1) * b->n] = (lo >> 16) | (hi & 0xffff0000u);
             } else {

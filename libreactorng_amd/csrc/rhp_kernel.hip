@@ -332,7 +332,10 @@ struct DevMove {
       partial(A);
       A += 16;
     }
-    constexpr int U = 4;
+#ifndef RHP_MOVE_UNROLL
+#define RHP_MOVE_UNROLL 4
+#endif
+    constexpr int U = RHP_MOVE_UNROLL;   /* destination blocks per memory round trip */
     while (A + 16 * U <= de) {
       const uintptr_t s0 = (A + delta) & ~(uintptr_t) 15;
       u32x4 l[U + 1];
@@ -520,41 +523,22 @@ __device__ __forceinline__ int http_frame_fast(const uint8_t *b, uint64_t len, i
   return kFrameDone;
 }
 
-/* The wave-cooperative payload move of chunked bodies (http.c:134-160, the
- * memmove of each chunk's data down to the running body end).  The replay's
- * threads validate their requests' chunks one per thread (the size lines are
- * a dependent walk) and leave each body's chunk list in LDS (a MoveTable per
- * lane); the wave then moves the bodies ONE AT A TIME WITH ALL 64 LANES: lane j
- * writes the j-th aligned 16-byte block of the de-framed body (and j + 64, ...),
- * built from the one or two chunks that block's bytes come from (two aligned
- * 16-byte source loads each, funnel-shifted by the chunk's own shift, merged by
- * a byte mask), so a wave store covers 1 KiB of contiguous lines and every
- * source line is fetched once, where the per-thread mover touched 64 different
- * lines per store and re-fetched each line per 16 bytes once L2 had evicted it
- * (4.1x the algorithmic bytes, profiles/r03/c).  Four bodies' loads are in
- * flight per round trip.  Bodies with more than kMoveChunks chunks, a chunk
- * shorter than 16 bytes (a block could then draw on three chunks) or offsets
- * past 4 GiB keep the per-thread mover. */
+/* A chunked body's de-framing (http_dechunk, http.c:134-160) by one thread:
+ * the validation pass walks the size lines once and keeps the first
+ * kMoveChunks chunks' data spans in registers, so the moves (DevMove, in
+ * order, each chunk's data down to the running body end) need no second walk
+ * of the size lines (dechunk_t's second pass; a body of more chunks still
+ * walks them again). */
 enum : uint32_t { kMoveChunks = 8 };
-struct MoveTable {   /* in LDS, one per lane of the replay's current batch */
-  uint64_t base;     /* the body's first byte (absolute address): the de-framed body goes to [base, base + len) */
-  uint32_t nch, len; /* data chunks, de-framed body length */
-  uint32_t src[kMoveChunks], n[kMoveChunks];   /* chunk c's data: [base + src[c], + n[c]) */
-};
-static_assert(sizeof(MoveTable) == 80, "MoveTable layout");
-
-/* validate a chunked body (dechunk_t's first pass) and, when it qualifies,
- * leave its moves in *t for the wave (true); otherwise it is finished here */
-__device__ __forceinline__ bool chunked_validate(uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x, bool compact,
-                                                 MoveTable *t)
+__device__ __forceinline__ void frame_chunked(uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x, bool compact)
 {
   rhp_http_t o = {1, compact ? 1u : (uint32_t) RHP_BODY_CHUNKED_PENDING, 0, 0};
   uint8_t *in = b + ret;
   const uint64_t size = len - (uint64_t) ret;
   LineBytes B{in, ~0ull, {0, 0, 0, 0}};
   uint64_t off = 0, doff = 0, dlen = 0, sum = 0;
-  uint32_t k = 0, src[kMoveChunks], n[kMoveChunks];
-  bool small = false;
+  uint32_t k = 0;
+  uint64_t src[kMoveChunks], n[kMoveChunks];
   int64_t res;
   do {
     res = one_chunk_t(B, off, size, &doff, &dlen);
@@ -562,8 +546,7 @@ __device__ __forceinline__ bool chunked_validate(uint8_t *b, uint64_t len, int32
     if (dlen) {
 #pragma unroll
       for (uint32_t j = 0; j < kMoveChunks; j++)
-        if (j == k) { src[j] = (uint32_t) (off + doff); n[j] = (uint32_t) dlen; }
-      small |= dlen < 16u;
+        if (j == k) { src[j] = off + doff; n[j] = dlen; }
       k++;
     }
     off += (uint64_t) res;
@@ -572,25 +555,24 @@ __device__ __forceinline__ bool chunked_validate(uint8_t *b, uint64_t len, int32
   if (res <= 0) {
     o.result = (int32_t) res;
     *x = o;
-    return false;
+    return;
   }
   o.body_len = sum;
   o.consumed = (uint64_t) ret + off;
   *x = o;
-  if (!compact) return false;
-  if (k <= kMoveChunks && !small && off <= 0xffffffffull) {
-    t->base = (uint64_t) (uintptr_t) in;
-    t->nch = k;
-    t->len = (uint32_t) sum;
+  if (!compact) return;
+  DevMove M{in};
+  if (k <= kMoveChunks) {
+    uint64_t total = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kMoveChunks; j++) {
-      t->src[j] = j < k ? src[j] : 0u;
-      t->n[j] = j < k ? n[j] : 0u;
+      if (j < k) {
+        M(total, src[j], n[j]);
+        total += n[j];
+      }
     }
-    return true;
+    return;
   }
-  /* the per-thread mover: dechunk_t's second pass */
-  DevMove M{in};
   uint64_t total = 0;
   off = 0;
   do {
@@ -599,147 +581,8 @@ __device__ __forceinline__ bool chunked_validate(uint8_t *b, uint64_t len, int32
     off += (uint64_t) res;
     total += dlen;
   } while (dlen);
-  return false;
 }
 
-/* the wave moves the bodies of the lanes in `m` (their MoveTables at tbl[lane]).
- * Branch-free up to the stores, so the R bodies' loads (two per chunk a block
- * draws on) all issue before the first wait: lanes with nothing to do load
- * the body's first line. */
-__device__ __forceinline__ void wave_moves(uint64_t m, const MoveTable *tbl, uint32_t lane)
-{
-  typedef __attribute__((address_space(1))) const u32x4 gq;
-  typedef __attribute__((address_space(1))) u32x4 gw;
-  typedef __attribute__((address_space(1))) uint8_t gb1;
-  typedef __attribute__((address_space(1))) uint32_t gw1;
-  constexpr int R = 2;   /* bodies per memory round trip */
-  while (m) {
-    int ln[R];
-#pragma unroll
-    for (int q = 0; q < R; q++) {
-      ln[q] = m ? (int) __builtin_ctzll(m) : -1;
-      m &= m ? m - 1 : 0ull;
-    }
-    uint64_t base[R];
-    uint32_t len[R], nch[R], groups[R], G = 0;
-#pragma unroll
-    for (int q = 0; q < R; q++) {
-      const MoveTable *t = tbl + (ln[q] < 0 ? 0 : ln[q]);
-      base[q] = t->base;
-      len[q] = ln[q] < 0 ? 0u : t->len;
-      nch[q] = t->nch;
-      const uint64_t a0 = base[q] & ~(uint64_t) 15, a1 = (base[q] + len[q] + 15u) & ~(uint64_t) 15;
-      groups[q] = len[q] ? (uint32_t) (((a1 - a0) / 16u + 63u) / 64u) : 0u;
-      G = max(G, groups[q]);
-    }
-    for (uint32_t g = 0; g < G; g++) {
-      uint64_t A[R], src[R][2];
-      int64_t t0[R];
-      uint32_t d[R][2], nc[R][2];
-      bool use[R][2];
-      u32x4 l[R][2][2];
-#pragma unroll
-      for (int q = 0; q < R; q++) {
-        const MoveTable *t = tbl + (ln[q] < 0 ? 0 : ln[q]);
-        A[q] = (base[q] & ~(uint64_t) 15) + 16u * ((uint64_t) g * 64u + lane);   /* this lane's destination block */
-        t0[q] = (int64_t) (A[q] - base[q]);                                      /* its first byte, body-relative */
-        const bool live = g < groups[q] && t0[q] < (int64_t) len[q];
-        /* the chunk holding the block's first body byte (chunk 0 for a partial
-         * first block), and the next one when the block runs past its end
-         * (every chunk is >= 16 B, so no block draws on a third) */
-        const int64_t tf = t0[q] < 0 ? 0 : t0[q];
-        uint32_t c = 0, dc = 0, de = t->n[0];
-#pragma unroll
-        for (uint32_t j = 1; j < kMoveChunks; j++) {
-          const bool past = j < nch[q] && (int64_t) de <= tf;
-          c = past ? j : c;
-          dc = past ? de : dc;
-          de += past ? t->n[j] : 0u;
-        }
-        const uint32_t c1 = c + 1u < kMoveChunks ? c + 1u : c;
-        use[q][0] = live;
-        use[q][1] = live && c + 1u < nch[q] && (int64_t) de < t0[q] + 16;
-        d[q][0] = dc;
-        d[q][1] = de;
-        nc[q][0] = t->n[c];
-        nc[q][1] = t->n[c1];
-        /* the source of body byte x of a chunk starting at body offset dc: base + src + (x - dc) */
-        src[q][0] = live ? A[q] + (uint64_t) t->src[c] - dc : base[q];
-        src[q][1] = use[q][1] ? A[q] + (uint64_t) t->src[c1] - de : base[q];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          const uint64_t sl = src[q][h] & ~(uint64_t) 15;
-          l[q][h][0] = *reinterpret_cast<gq *>((uintptr_t) sl);
-          l[q][h][1] = *reinterpret_cast<gq *>((uintptr_t) sl + 16);
-        }
-      }
-      /* every load of the round trip has landed before any store: a store
-       * never overwrites a source byte another lane still reads (each block's
-       * source lies at or past its destination) */
-#pragma unroll
-      for (int q = 0; q < R; q++) {
-        u32x4 v[2];
-        uint32_t msk[2];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          const uint32_t qd = (uint32_t) (src[q][h] >> 2) & 3u, r = (uint32_t) src[q][h] & 3u;
-          const uint32_t w[8] = {l[q][h][0][0], l[q][h][0][1], l[q][h][0][2], l[q][h][0][3],
-                                 l[q][h][1][0], l[q][h][1][1], l[q][h][1][2], l[q][h][1][3]};
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const uint32_t lo = qd == 0 ? w[j] : qd == 1 ? w[j + 1] : qd == 2 ? w[j + 2] : w[j + 3];
-            const uint32_t hi = qd == 0 ? w[j + 1] : qd == 1 ? w[j + 2] : qd == 2 ? w[j + 3] : w[j + 4];
-            v[h][j] = __builtin_amdgcn_alignbyte(hi, lo, r);
-          }
-          /* the block's bytes inside the chunk: body offsets [d, d + n) */
-          const int64_t lo_b = (int64_t) d[q][h] - t0[q], hi_b = (int64_t) (d[q][h] + nc[q][h]) - t0[q];
-          const uint32_t lo_c = (uint32_t) (lo_b < 0 ? 0 : lo_b > 16 ? 16 : lo_b);
-          const uint32_t hi_c = (uint32_t) (hi_b < 0 ? 0 : hi_b > 16 ? 16 : hi_b);
-          msk[h] = use[q][h] && hi_c > lo_c ? ((0xffffu >> (16u - (hi_c - lo_c))) << lo_c) & 0xffffu : 0u;
-        }
-        const uint32_t keep = msk[0] | msk[1];
-        u32x4 out;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const uint32_t b1 = (msk[1] >> (4 * j)) & 15u;
-          const uint32_t sel = (b1 & 1u ? 0xffu : 0u) | (b1 & 2u ? 0xff00u : 0u) | (b1 & 4u ? 0xff0000u : 0u) |
-                               (b1 & 8u ? 0xff000000u : 0u);
-          out[j] = (v[1][j] & sel) | (v[0][j] & ~sel);
-        }
-        if (keep == 0xffffu) {
-          *reinterpret_cast<gw *>((uintptr_t) A[q]) = out;
-        } else if (keep) {   /* a partial first or last block: only the body's bytes */
-#pragma unroll
-          for (uint32_t j = 0; j < 4; j++) {
-            const uint32_t kb = (keep >> (4 * j)) & 15u;
-            if (kb == 15u) {
-              *reinterpret_cast<gw1 *>((uintptr_t) A[q] + 4 * j) = out[j];
-            } else if (kb) {
-#pragma unroll
-              for (uint32_t z = 0; z < 4; z++)
-                if (kb >> z & 1u) *reinterpret_cast<gb1 *>((uintptr_t) A[q] + 4 * j + z) = (uint8_t) (out[j] >> (8 * z));
-            }
-          }
-        }
-      }
-    }
-  }
-}
-
-/* the chunked body of a request whose framing http_frame_fast settled
- * (kFrameChunked): http_dechunk over (ret, len), http.c:225-230 */
-__device__ __forceinline__ void frame_chunked(uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x, bool compact)
-{
-  rhp_http_t o = {1, compact ? 1u : (uint32_t) RHP_BODY_CHUNKED_PENDING, 0, 0};
-  uint64_t blen = 0;
-  const int64_t size = DevDechunk{}(b + ret, len - (uint64_t) ret, &blen, compact);
-  if (size <= 0) {
-    o.result = (int32_t) size; o.body_kind = 0;
-  } else {
-    o.body_len = blen; o.consumed = (uint64_t) ret + (uint64_t) size;
-  }
-  *x = o;
-}
 
 /* Params pointers are generic in the kernel's view (they sit in a struct);
  * the hot stores go through explicit global-address-space pointers so they are
@@ -1767,11 +1610,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     };
     uint32_t *slow = reinterpret_cast<uint32_t *>(lds + kLdsTable);   /* the staging area, idle now */
     uint32_t *slow_n = wg_counter + 4;                                 /* 0 since the prologue */
-    /* the staging area's end holds each wave's MoveTables (wave_moves) */
-    constexpr uint32_t kMoveBytes = 64u * sizeof(MoveTable);
-    constexpr uint32_t kSlowCap = WAVES * (kStageWave - kMoveBytes) / 4;
-    static_assert(kStageWave > kMoveBytes, "a wave's move tables fit its share of the staging area");
-    MoveTable *moves = reinterpret_cast<MoveTable *>(lds + kLdsTable + 4u * kSlowCap) + (tid >> 6) * 64u;
+    constexpr uint32_t kSlowCap = WAVES * kStageWave / 4;
     dg.pass_begin();
     /* the deferred requests: the list finalize kept, or the whole range when
      * it overflowed */
@@ -1805,26 +1644,14 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     __syncthreads();
     dg.pass_begin();
     const uint32_t ns = min(*slow_n, kSlowCap);
-    /* wave-uniform trips: the chunked bodies' payloads are moved by the whole
-     * wave once its lanes have validated them (wave_moves) */
-    for (uint32_t kb = tid & ~63u; kb < ns; kb += WAVES * 64) {
-      const uint32_t k = kb + lane;
-      bool coop = false;
-      if (k < ns) {
-        const uint32_t e = slow[k], i = wg_lo + (e & 0x7fffffffu);
-        const Head h = head(i);
-        if (http && (e >> 31))   /* chunked bodies: http mode only */
-          coop = chunked_validate(p.bytes_rw + h.off, h.end - h.off, (int32_t) (h.hint[1] & 0xffffu), &p.http[i],
-                                  p.compact, moves + lane);
-        else
-          finish_slow(i, h);
-        dg.slow_path();
-      }
-      const uint64_t m = __builtin_amdgcn_ballot_w64(coop);
-      if (http && m) {
-        wait_lgkm0();   /* the lanes' tables are in LDS (a wave reads its own) */
-        wave_moves(m, moves, lane);
-      }
+    for (uint32_t k = tid; k < ns; k += WAVES * 64) {
+      const uint32_t e = slow[k], i = wg_lo + (e & 0x7fffffffu);
+      const Head h = head(i);
+      if (http && (e >> 31))   /* chunked bodies: http mode only */
+        frame_chunked(p.bytes_rw + h.off, h.end - h.off, (int32_t) (h.hint[1] & 0xffffu), &p.http[i], p.compact);
+      else
+        finish_slow(i, h);
+      dg.slow_path();
     }
     dg.pass_end(0);
   }

@@ -16,6 +16,7 @@ pp = d.get("pipelined", {}).get("ms_per_step")
 print(f"{sys.argv[1]:10s} c2 {d['roofline']['kernel_ms']*1e3:7.1f} us (frac {d['roofline']['frac']:.3f}, wall {d['ms_per_step']*1e3:6.1f} us"
       + (f", 2 streams {pp*1e3:6.1f} us" if pp else "") + ")  "
       f"c3 {e.get('zipf', {}).get('roofline', {}).get('kernel_ms', 0)*1e3:7.1f} us  c5 {e.get('post', {}).get('roofline', {}).get('kernel_ms', 0)*1e3:7.1f} us  "
+      f"chunked {e.get('chunked', {}).get('roofline', {}).get('kernel_ms', 0)*1e3:7.1f} us  "
       f"ok {d['config']['ok_fraction']:.3f}  parity {sorted(set(d.get('parity', {}).values()))}")
 PY
   done

@@ -59,9 +59,10 @@
 #define RHP_BLOCK 64
 #endif
 /* http mode's window extension in 16-byte parts: its windows are RHP_BLOCK +
- * 16 * RHP_HTTP_XPARTS bytes (rhp_kernel.hip, window geometry) */
+ * 16 * RHP_HTTP_XPARTS bytes (rhp_kernel.hip, window geometry; measured with 2
+ * and not kept) */
 #ifndef RHP_HTTP_XPARTS
-#define RHP_HTTP_XPARTS 2
+#define RHP_HTTP_XPARTS 0
 #endif
 #define RHP_HTTP_BLOCK (RHP_BLOCK + 16 * RHP_HTTP_XPARTS)
 

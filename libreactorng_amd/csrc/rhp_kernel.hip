@@ -692,14 +692,16 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 
   const uint32_t maxh = p.max_headers;
   constexpr bool http = HTTP;   /* p.mode == RHP_MODE_HTTP (the launch picks the instance) */
-  /* Window geometry.  The early form walks 128-byte windows (whole HBM lines);
-   * the http form's windows are kXParts 16-byte parts longer (kHttpXParts):
-   * the bytes of the next line a header section most often still needs, so
-   * a request whose header section fits (config 5: 133 B) is walked, decoded
-   * and framed in ONE iteration where 128 B took two -- the second for the
-   * few bytes up to its CRLFCRLF.  The extension parts go to a staging area of
-   * their own (xstage: part 8 + k of every lane's window at 1024 k + 16 lane),
-   * fetched by kXParts more LDS-DMA loads per issue. */
+  /* Window geometry.  Windows are 128 bytes (whole HBM lines).  The http form
+   * can walk kHttpXParts 16-byte parts more (RHP_HTTP_XPARTS, rhp_dfa.h), so a
+   * header section that fits (config 5: 133 B) is walked, decoded and framed in
+   * one iteration where 128 B takes two; the extension parts go to a staging
+   * area of their own (xstage: part 8 + k of every lane's window at 1024 k +
+   * 16 lane), fetched by kXParts more LDS-DMA loads per issue, and the
+   * staging leaves room for 12 waves.  Measured with 2 parts (160 B,
+   * profiles/r04/e/): config 5 +2-4 % (the fewer waves cost more than the
+   * iterations saved) and no fewer bytes fetched (the 32 B of the next line
+   * cost its whole line), so the default is 0. */
   constexpr uint32_t kXParts = (LATE && HTTP) ? kHttpXParts : 0u;
   constexpr uint32_t kWParts = kParts + kXParts;   /* 16-byte parts per window */
   constexpr uint32_t kWBlock = 16u * kWParts;      /* window bytes */

@@ -523,22 +523,32 @@ __device__ __forceinline__ int http_frame_fast(const uint8_t *b, uint64_t len, i
   return kFrameDone;
 }
 
-/* A chunked body's de-framing (http_dechunk, http.c:134-160) by one thread:
- * the validation pass walks the size lines once and keeps the first
- * kMoveChunks chunks' data spans in registers, so the moves (DevMove, in
- * order, each chunk's data down to the running body end) need no second walk
- * of the size lines (dechunk_t's second pass; a body of more chunks still
- * walks them again). */
-enum : uint32_t { kMoveChunks = 8 };
-__device__ __forceinline__ void frame_chunked(uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x, bool compact)
+/* A chunked body's de-framing (http_dechunk, http.c:134-160).  One thread
+ * validates it (the size lines are a dependent walk) and keeps the first
+ * kMoveChunks chunks' data spans in registers.  The payload moves -- each
+ * chunk's data down to the running body end, in order -- then go one of two
+ * ways:
+ *  - staged by the wave (staged_moves, below), when the body has at most
+ *    kMoveChunks chunks and its framed bytes fit a kStageBody slot: the
+ *    function leaves the spans in *sb and returns true;
+ *  - by this thread (DevMove from the kept spans, or from a second walk of
+ *    the size lines for a body of more chunks), returning false. */
+enum : uint32_t { kMoveChunks = 8, kStageBody = 2048, kStageBodies = 4 };
+struct StagedBody {
+  uint64_t base;           /* the body's first byte: the de-framed body goes to [base, base + len) */
+  uint32_t nch, region;    /* data chunks; framed bytes up to the last data byte */
+  uint32_t span[kMoveChunks];   /* chunk c's data: [base + (span & 0xffff), + (span >> 16)) (< kStageBody) */
+};
+__device__ __forceinline__ bool frame_chunked(uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x, bool compact,
+                                              StagedBody *sb = nullptr)
 {
   rhp_http_t o = {1, compact ? 1u : (uint32_t) RHP_BODY_CHUNKED_PENDING, 0, 0};
   uint8_t *in = b + ret;
   const uint64_t size = len - (uint64_t) ret;
   LineBytes B{in, ~0ull, {0, 0, 0, 0}};
-  uint64_t off = 0, doff = 0, dlen = 0, sum = 0;
+  uint64_t off = 0, doff = 0, dlen = 0, sum = 0, region = 0;
   uint32_t k = 0;
-  uint64_t src[kMoveChunks], n[kMoveChunks];
+  uint32_t src[kMoveChunks], n[kMoveChunks];   /* kept while the spans stay below 4 GiB (region) */
   int64_t res;
   do {
     res = one_chunk_t(B, off, size, &doff, &dlen);
@@ -546,8 +556,9 @@ __device__ __forceinline__ void frame_chunked(uint8_t *b, uint64_t len, int32_t 
     if (dlen) {
 #pragma unroll
       for (uint32_t j = 0; j < kMoveChunks; j++)
-        if (j == k) { src[j] = off + doff; n[j] = dlen; }
+        if (j == k) { src[j] = (uint32_t) (off + doff); n[j] = (uint32_t) dlen; }
       k++;
+      region = off + doff + dlen;
     }
     off += (uint64_t) res;
     sum += dlen;
@@ -555,14 +566,22 @@ __device__ __forceinline__ void frame_chunked(uint8_t *b, uint64_t len, int32_t 
   if (res <= 0) {
     o.result = (int32_t) res;
     *x = o;
-    return;
+    return false;
   }
   o.body_len = sum;
   o.consumed = (uint64_t) ret + off;
   *x = o;
-  if (!compact) return;
+  if (!compact) return false;
+  if (sb && k <= kMoveChunks && region + 16u <= kStageBody) {
+    sb->base = (uint64_t) (uintptr_t) in;
+    sb->nch = k;
+    sb->region = (uint32_t) region;
+#pragma unroll
+    for (uint32_t j = 0; j < kMoveChunks; j++) sb->span[j] = j < k ? (uint32_t) src[j] | (uint32_t) n[j] << 16 : 0u;
+    return true;
+  }
   DevMove M{in};
-  if (k <= kMoveChunks) {
+  if (k <= kMoveChunks && region <= 0xffffffffull) {
     uint64_t total = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kMoveChunks; j++) {
@@ -571,7 +590,7 @@ __device__ __forceinline__ void frame_chunked(uint8_t *b, uint64_t len, int32_t 
         total += n[j];
       }
     }
-    return;
+    return false;
   }
   uint64_t total = 0;
   off = 0;
@@ -581,6 +600,135 @@ __device__ __forceinline__ void frame_chunked(uint8_t *b, uint64_t len, int32_t 
     off += (uint64_t) res;
     total += dlen;
   } while (dlen);
+  return false;
+}
+
+/* The wave's payload moves for the bodies of the lanes in `m` (their spans in
+ * those lanes' *sb), kStageBodies bodies per memory round trip:
+ *  1. the wave loads each body's framed bytes [base & ~15, base + region) as
+ *     whole 16-byte lines, 64 lanes side by side (1 KiB per instruction, every
+ *     line fetched once), and writes them to the body's LDS slot;
+ *  2. lane j then builds the j-th 16-byte block of the de-framed body from LDS
+ *     -- for each chunk the block draws on, two aligned ds_read_b128 funnel-
+ *     shifted by that chunk's offset and merged by a byte mask -- and stores it:
+ *     1 KiB of contiguous lines per wave store, only the body's bytes in the
+ *     first and last block.
+ * Every global load of a round trip lands before its stores (each chunk's
+ * data lies at or past its destination, and bodies do not overlap).  The
+ * per-thread mover this replaces wrote 16 bytes of 64 different lines per
+ * store and fetched each line again once L2 had evicted it (config "chunked":
+ * 4.1x the algorithmic bytes, profiles/r03/c/). */
+__device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, uint32_t lane, uint32_t stage)
+{
+  typedef __attribute__((address_space(1))) const u32x4 gq;
+  typedef __attribute__((address_space(1))) u32x4 gw;
+  typedef __attribute__((address_space(1))) uint8_t gb1;
+  typedef __attribute__((address_space(1))) uint32_t gw1;
+  typedef __attribute__((address_space(3))) u32x4 lq;
+  constexpr uint32_t kLinesPerLane = kStageBody / 1024u;   /* 16-byte lines per lane per body */
+  while (m) {
+    /* the next kStageBodies bodies: their spans from their lanes (scalar) */
+    uint32_t owner[kStageBodies];
+    bool have[kStageBodies];
+#pragma unroll
+    for (uint32_t q = 0; q < kStageBodies; q++) {
+      have[q] = m != 0;
+      owner[q] = m ? (uint32_t) __builtin_ctzll(m) : owner[0];
+      m &= m ? m - 1 : 0ull;
+    }
+    uint64_t base[kStageBodies];
+    uint32_t region[kStageBodies];
+#pragma unroll
+    for (uint32_t q = 0; q < kStageBodies; q++) {
+      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t) sb.base, owner[q]);
+      const uint32_t hi = __builtin_amdgcn_readlane((uint32_t) (sb.base >> 32), owner[q]);
+      base[q] = (uint64_t) lo | (uint64_t) hi << 32;
+      region[q] = have[q] ? __builtin_amdgcn_readlane(sb.region, owner[q]) : 0u;
+    }
+    /* 1. framed bytes -> LDS (lines past a body's region load its first line) */
+    u32x4 raw[kStageBodies][kLinesPerLane];
+#pragma unroll
+    for (uint32_t q = 0; q < kStageBodies; q++) {
+      const uint64_t la = base[q] & ~(uint64_t) 15;
+      const uint32_t lines = (uint32_t) ((base[q] + region[q] + 15u - la) >> 4);
+#pragma unroll
+      for (uint32_t h = 0; h < kLinesPerLane; h++) {
+        const uint32_t line = lane + 64u * h;
+        raw[q][h] = *reinterpret_cast<gq *>((uintptr_t) (la + (line < lines ? 16u * line : 0u)));
+      }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kStageBodies; q++)
+#pragma unroll
+      for (uint32_t h = 0; h < kLinesPerLane; h++)
+        *reinterpret_cast<lq *>((size_t) (stage + kStageBody * q + 16u * (lane + 64u * h))) = raw[q][h];
+    wait_lgkm0();   /* the wave's slots are written (a wave reads its own) */
+    /* 2. the de-framed blocks */
+#pragma unroll
+    for (uint32_t q = 0; q < kStageBodies; q++) {
+      if (!have[q]) continue;
+      const uint32_t nch = __builtin_amdgcn_readlane(sb.nch, owner[q]);
+      uint32_t cs[kMoveChunks], cn[kMoveChunks], cd[kMoveChunks + 1];   /* span, length, body offset (scalar) */
+      cd[0] = 0;
+#pragma unroll
+      for (uint32_t c = 0; c < kMoveChunks; c++) {
+        const uint32_t sp = __builtin_amdgcn_readlane(sb.span[c], owner[q]);
+        cs[c] = sp & 0xffffu;
+        cn[c] = sp >> 16;
+        cd[c + 1] = cd[c] + cn[c];
+      }
+      const uint32_t L = cd[kMoveChunks];   /* spans past nch are empty */
+      const uint64_t a0 = base[q] & ~(uint64_t) 15;
+      const uint32_t lead = (uint32_t) (base[q] - a0);   /* the body's first byte inside its first line */
+      const uint32_t blocks = (lead + L + 15u) >> 4;
+      for (uint32_t b = lane; b < blocks; b += 64u) {
+        /* block b covers body offsets [t0, t0 + 16), t0 = 16 b - lead */
+        const int32_t t0 = (int32_t) (16u * b) - (int32_t) lead;
+        u32x4 out = u32x4{0, 0, 0, 0};
+        uint32_t keep = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < kMoveChunks; c++) {
+          const int32_t lo_b = (int32_t) cd[c] - t0, hi_b = (int32_t) cd[c + 1] - t0;
+          if (c >= nch || hi_b <= 0 || lo_b >= 16) continue;   /* the block draws nothing from chunk c */
+          /* body byte x of chunk c lies at LDS slot offset lead + cs[c] + (x - cd[c]) */
+          const uint32_t P = (uint32_t) ((int32_t) (lead + cs[c]) + t0 - (int32_t) cd[c]);
+          const uint32_t pl = stage + kStageBody * q + (P & ~15u);
+          const u32x4 l0 = *reinterpret_cast<const lq *>((size_t) pl), l1 = *reinterpret_cast<const lq *>((size_t) pl + 16u);
+          const uint32_t qd = (P >> 2) & 3u, r = P & 3u;
+          const uint32_t w[8] = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+          const uint32_t lo_c = lo_b < 0 ? 0u : (uint32_t) lo_b, hi_c = hi_b > 16 ? 16u : (uint32_t) hi_b;
+          const uint32_t msk = ((0xffffu >> (16u - (hi_c - lo_c))) << lo_c) & 0xffffu;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const uint32_t lo = qd == 0 ? w[j] : qd == 1 ? w[j + 1] : qd == 2 ? w[j + 2] : w[j + 3];
+            const uint32_t hi = qd == 0 ? w[j + 1] : qd == 1 ? w[j + 2] : qd == 2 ? w[j + 3] : w[j + 4];
+            const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, r);
+            const uint32_t bm = (msk >> (4 * j)) & 15u;
+            const uint32_t sel = (bm & 1u ? 0xffu : 0u) | (bm & 2u ? 0xff00u : 0u) | (bm & 4u ? 0xff0000u : 0u) |
+                                 (bm & 8u ? 0xff000000u : 0u);
+            out[j] = (v & sel) | (out[j] & ~sel);
+          }
+          keep |= msk;
+        }
+        const uintptr_t A = (uintptr_t) (a0 + 16u * b);
+        if (keep == 0xffffu) {
+          *reinterpret_cast<gw *>(A) = out;
+        } else if (keep) {   /* the body's first or last block: only its bytes */
+#pragma unroll
+          for (uint32_t j = 0; j < 4; j++) {
+            const uint32_t kb = (keep >> (4 * j)) & 15u;
+            if (kb == 15u) {
+              *reinterpret_cast<gw1 *>(A + 4 * j) = out[j];
+            } else if (kb) {
+#pragma unroll
+              for (uint32_t z = 0; z < 4; z++)
+                if (kb >> z & 1u) *reinterpret_cast<gb1 *>(A + 4 * j + z) = (uint8_t) (out[j] >> (8 * z));
+            }
+          }
+        }
+      }
+    }
+  }
 }
 
 
@@ -1610,9 +1758,12 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
                    &p.http[i], (cand >> 31) ? ~0ull : (uint64_t) (cand & 0x3fffffffu), p.compact, DevDechunk{});
       }
     };
-    uint32_t *slow = reinterpret_cast<uint32_t *>(lds + kLdsTable);   /* the staging area, idle now */
+    /* the list lives where the DFA table was (idle now); the staging area
+     * holds the chunked bodies' LDS slots (staged_moves) */
+    uint32_t *slow = reinterpret_cast<uint32_t *>(lds);
     uint32_t *slow_n = wg_counter + 4;                                 /* 0 since the prologue */
-    constexpr uint32_t kSlowCap = WAVES * kStageWave / 4;
+    constexpr uint32_t kSlowCap = kLdsTable / 4;
+    static_assert(kStageBody * kStageBodies <= kStageWave, "a wave's body slots fit its staging");
     dg.pass_begin();
     /* the deferred requests: the list finalize kept, or the whole range when
      * it overflowed */
@@ -1646,14 +1797,26 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     __syncthreads();
     dg.pass_begin();
     const uint32_t ns = min(*slow_n, kSlowCap);
-    for (uint32_t k = tid; k < ns; k += WAVES * 64) {
-      const uint32_t e = slow[k], i = wg_lo + (e & 0x7fffffffu);
-      const Head h = head(i);
-      if (http && (e >> 31))   /* chunked bodies: http mode only */
-        frame_chunked(p.bytes_rw + h.off, h.end - h.off, (int32_t) (h.hint[1] & 0xffffu), &p.http[i], p.compact);
-      else
-        finish_slow(i, h);
-      dg.slow_path();
+    /* wave-uniform trips: the chunked bodies its lanes validated are moved by
+     * the whole wave (staged_moves) */
+    for (uint32_t kb = tid & ~63u; kb < ns; kb += WAVES * 64) {
+      const uint32_t k = kb + lane;
+      StagedBody sb;
+      bool staged = false;
+      if (k < ns) {
+        const uint32_t e = slow[k], i = wg_lo + (e & 0x7fffffffu);
+        const Head h = head(i);
+        if (http && (e >> 31))   /* chunked bodies: http mode only */
+          staged = frame_chunked(p.bytes_rw + h.off, h.end - h.off, (int32_t) (h.hint[1] & 0xffffu), &p.http[i],
+                                 p.compact, &sb);
+        else
+          finish_slow(i, h);
+        dg.slow_path();
+      }
+      if (http) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64(staged);
+        if (m) staged_moves(m, sb, lane, stage);
+      }
     }
     dg.pass_end(0);
   }

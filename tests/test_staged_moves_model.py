@@ -1,0 +1,92 @@
+"""A CPU model of rhp_kernel.hip's staged_moves -- the wave's payload moves of
+chunked bodies (http.c:134-160, the memmove of each chunk's data down to the
+running body end): per body the framed bytes as 16-byte lines into an LDS slot,
+then per lane the 16-byte block of the de-framed body built from the slot, one
+funnel-shifted pair of 16-byte slot reads per chunk the block draws on, merged
+by byte masks.  The same arithmetic, lane by lane, over the chunked workload's
+bodies that the kernel stages (<= 8 chunks, framed bytes + 16 <= 2048): the
+blocks rebuild exactly the oracle's de-framed bytes, every global load stays
+inside the body's framed lines, every slot read inside the slot (+ the 32-byte
+overhang the kernel tolerates) and no store leaves the body.  The GPU tests
+check the kernel itself (golden sets and the full-size digest)."""
+import numpy as np
+
+import libreactorng_amd as rhp
+from oracle_util import run_oracle
+
+K_MOVE_CHUNKS, K_STAGE_BODY = 8, 2048
+
+
+def chunk_spans(buf, start, end):
+    """[(src, n)] data spans (body-relative) and the framed length up to the last data byte,
+    as one_chunk_t walks a valid body"""
+    at, out, region = start, [], 0
+    while True:
+        nl = bytes(buf[at:end]).index(b"\n")
+        size = int(bytes(buf[at:at + nl + 1]).split(b";")[0].strip(b" \t\r\n"), 16)
+        data = at + nl + 1
+        if size == 0:
+            return out, region
+        out.append((data - start, size))
+        region = data - start + size
+        at = data + size + 2
+
+
+def staged_body(buf, base, spans, region):
+    """one body: returns the (address, byte) stores and checks every access"""
+    la = base & ~15
+    lines = (base + region + 15 - la) >> 4
+    assert lines <= 128
+    slot = bytearray(K_STAGE_BODY + 64)
+    for lane in range(64):
+        for h in range(2):
+            line = lane + 64 * h
+            a = la + (16 * line if line < lines else 0)
+            assert la <= a and a + 16 <= la + 16 * max(lines, 1), "a global load outside the body's lines"
+            slot[16 * line:16 * line + 16] = bytes(buf[a:a + 16])
+    cd = [0]
+    for _, n in spans:
+        cd.append(cd[-1] + n)
+    L, lead = cd[-1], base - la
+    stores = []
+    for b in range((lead + L + 15) >> 4):
+        t0 = 16 * b - lead
+        out, keep = bytearray(16), [False] * 16
+        for c, (cs, n) in enumerate(spans):
+            lo_b, hi_b = cd[c] - t0, cd[c + 1] - t0
+            if hi_b <= 0 or lo_b >= 16:
+                continue
+            P = lead + cs + t0 - cd[c]
+            assert 0 <= P and (P & ~15) + 32 <= K_STAGE_BODY + 48, "a slot read outside the slot"
+            v = slot[P:P + 16]
+            for k in range(max(lo_b, 0), min(hi_b, 16)):
+                out[k] = v[k]
+                keep[k] = True
+        A = la + 16 * b
+        for k in range(16):
+            if keep[k]:
+                assert base <= A + k < base + L, "a store outside the body"
+                stores.append((A + k, out[k]))
+    return stores
+
+
+def test_staged_moves_model_matches_oracle():
+    n = 2048
+    buf, off = rhp.generate(rhp.GEN_CHUNKED, n, 4242)
+    reqs, _, http, want = run_oracle(buf, off, 16, rhp.MODE_HTTP)
+    work = buf.copy()
+    staged = 0
+    for i in range(n):
+        if http["result"][i] != 1 or not http["body_kind"][i]:
+            continue
+        base, end = int(off[i]) + int(reqs["ret"][i]), int(off[i + 1])
+        spans, region = chunk_spans(buf, base, end)
+        L = sum(x for _, x in spans)
+        if len(spans) > K_MOVE_CHUNKS or region + 16 > K_STAGE_BODY:
+            work[base:base + L] = want[base:base + L]   # the kernel's per-thread mover
+            continue
+        staged += 1
+        for a, v in staged_body(buf, base, spans, region):   # every load before any store (one body)
+            work[a] = v
+    assert staged > n * 0.8
+    assert np.array_equal(work, want), f"{int((work != want).sum())} bytes differ from the oracle's"

@@ -343,6 +343,7 @@ class GpuRunner:
         for e in ends:
             self.stream.wait_event(e)
         torch.cuda.synchronize()
+        self.nstep = steps   # last_result: the outputs of launch steps - 1
         return time.perf_counter() - t0
 
     def last_result(self):
@@ -427,7 +428,7 @@ def golden_spec(key, lo, n):
     return None
 
 
-def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
+def run_config(key, args, rank, world, per_gpu, steps, warmup, dist, streams=1):
     cfg = CONFIGS[key]
     n_total = per_gpu * world
     lo, hi = shard_range(n_total, rank, world)
@@ -436,7 +437,9 @@ def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
     lay_name = cfg["layout"] if args.layout == "auto" or (args.layout == "compact" and cfg["mode"] != rhp.MODE_PHR) \
         else args.layout
     layout = LAYOUTS[lay_name]
-    runner = (EmuRunner if args.device == "cpu" else GpuRunner)(cfg, lo, hi, args.copies, layout)
+    streams = streams if args.device == "gpu" and not cfg.get("rewrites") else 1
+    runner = (GpuRunner(cfg, lo, hi, max(args.copies, streams), layout, streams=streams) if args.device == "gpu"
+              else EmuRunner(cfg, lo, hi, args.copies, layout))
     for k in range(warmup):
         runner.step(k)
     runner.sync()
@@ -447,14 +450,18 @@ def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
     wall, kern_ms = runner.timed(steps)
     if dist is not None:
         dist.barrier()
-    piped = None
-    if args.pipeline_streams > 1 and args.device == "gpu" and not cfg.get("rewrites"):
-        pr = GpuRunner(cfg, lo, hi, max(args.copies, args.pipeline_streams), layout, streams=args.pipeline_streams)
-        pr.timed_pipelined(warmup)
-        pw = pr.timed_pipelined(steps)
-        piped = {"streams": args.pipeline_streams, "ms_per_step": round(pw * 1e3 / steps, 4),
-                 "value": round(float(alg_bytes) * steps / pw / 2 ** 30, 2)}
-        del pr
+    single = None
+    if streams > 1:
+        # the same K steps with the batches alternating over `streams` HIP streams: the
+        # value's timed region (the single-stream one above gives the kernel time)
+        single = wall
+        runner.timed_pipelined(warmup)
+        if dist is not None:
+            dist.barrier()
+        runner.sync()
+        wall = runner.timed_pipelined(steps)
+        if dist is not None:
+            dist.barrier()
     # outside the timed region: the last timed launch's records against the reference's digest
     spec = golden_spec(key, lo, hi - lo)
     parity = runner.parity(spec)
@@ -464,9 +471,10 @@ def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
     total_alg = float(alg_bytes)
     if dist is not None:
         import torch
-        t = torch.tensor([wall, kern_ms], dtype=torch.float64)
+        t = torch.tensor([wall, kern_ms, single or 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, kern_ms = float(t[0]), float(t[1])
+        single = float(t[2]) if single is not None else None
         tb = torch.tensor([float(alg_bytes)], dtype=torch.float64)
         dist.all_reduce(tb)
         total_alg = float(tb[0])
@@ -482,7 +490,7 @@ def run_config(key, args, rank, world, per_gpu, steps, warmup, dist):
                 else parity_entry["result"]
     return dict(cfg=cfg, lo=lo, hi=hi, n_total=n_total, alg_bytes=alg_bytes, total_alg=total_alg, wall=wall,
                 kern_ms=kern_ms, ok_frac=ok_frac, steps=steps, warmup=warmup, parity=parity_entry, layout=lay_name,
-                pipelined=piped)
+                streams=streams, single_wall=single)
 
 
 def roofline(r, key):
@@ -508,9 +516,11 @@ def main(argv=None):
     ap.add_argument("--per-gpu", type=int, default=0, help="requests per GPU (default: the config's 1M)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory end-to-end leg")
-    ap.add_argument("--pipeline-streams", type=int, default=0,
-                    help="also time the config's batches alternating over this many HIP streams (two or more "
-                         "batches in flight, as the reactor's slots), reported beside the single-stream value")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the timed batches of the main config alternate over (`value`): two batches "
+                         "in flight, as the reactor's two slots, so one batch's tail overlaps the next one's start; "
+                         "1 = one stream.  The single-stream rate and the per-launch kernel time (roofline) are "
+                         "measured too, on one stream")
     ap.add_argument("--impl", type=int, default=rhp.IMPL_DFA)
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--layout", default="auto", choices=["auto"] + sorted(LAYOUTS),
@@ -539,7 +549,7 @@ def main(argv=None):
         rhp.lib().rhp_set_impl(args.impl)
     per_gpu = args.per_gpu or CONFIGS[args.config]["per_gpu"]
 
-    r = run_config(args.config, args, rank, world, per_gpu, args.steps, args.warmup, dist)
+    r = run_config(args.config, args, rank, world, per_gpu, args.steps, args.warmup, dist, streams=max(1, args.streams))
     extra = {}
     if world == 1 and args.extra == "auto" and args.config == "get256":
         for key in [k for k in args.extras.split(",") if k in EXTRA_KEYS]:
@@ -578,8 +588,11 @@ def main(argv=None):
         line["parity"].update({k: v["parity"]["result"] for k, v in extra.items()})
         line["parity_detail"] = {args.config: r["parity"], **{k: v["parity"] for k, v in extra.items()}}
         line["library_sha256"] = rhp.library_sha256() if args.device == "gpu" else None
-        if r.get("pipelined"):
-            line["pipelined"] = r["pipelined"]
+        line["batches_in_flight"] = r["streams"]
+        if r.get("single_wall") is not None:
+            line["single_stream"] = {"value": round(r["total_alg"] * r["steps"] / r["single_wall"] / 2 ** 30, 2),
+                                     "ms_per_step": round(r["single_wall"] * 1e3 / r["steps"], 4),
+                                     "note": "the same K steps on one HIP stream (one batch at a time)"}
         if extra:
             line["extra_configs"] = extra
         if world == 1 and args.device == "gpu" and not args.no_e2e:

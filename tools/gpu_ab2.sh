@@ -12,9 +12,9 @@ for r in $(seq 1 ${ROUNDS:-2}); do
 import json, sys
 d = json.load(open(f"gpurun_out/ab_{sys.argv[1]}.json"))
 e = d.get("extra_configs", {})
-pp = d.get("pipelined", {}).get("ms_per_step")
+ss = d.get("single_stream", {}).get("ms_per_step")
 print(f"{sys.argv[1]:10s} c2 {d['roofline']['kernel_ms']*1e3:7.1f} us (frac {d['roofline']['frac']:.3f}, wall {d['ms_per_step']*1e3:6.1f} us"
-      + (f", 2 streams {pp*1e3:6.1f} us" if pp else "") + ")  "
+      + f" x{d.get('batches_in_flight', 1)}" + (f", one stream {ss*1e3:6.1f} us" if ss else "") + ")  "
       f"c3 {e.get('zipf', {}).get('roofline', {}).get('kernel_ms', 0)*1e3:7.1f} us  c5 {e.get('post', {}).get('roofline', {}).get('kernel_ms', 0)*1e3:7.1f} us  "
       f"chunked {e.get('chunked', {}).get('roofline', {}).get('kernel_ms', 0)*1e3:7.1f} us  "
       f"ok {d['config']['ok_fraction']:.3f}  parity {sorted(set(d.get('parity', {}).values()))}")

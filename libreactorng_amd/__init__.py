@@ -64,7 +64,7 @@ RHP_SYMBOLS = ("rhp_parse_batch", "rhp_set_impl", "rhp_kernel_name", "rhp_versio
                "rhp_fixup_sessions")
 HOST_SYMBOLS = ("rhp_gen_size", "rhp_gen_fill", "rhp_gen_header_bytes", "rhp_splitmix64",
                 "rhp_emu_parse_batch", "rhp_cpu_parse_batch", "rhp_phr_parse_request", "rhp_http_read_cpu",
-                "rhp_cpu_fixup_sessions", "rhp_expand_records")
+                "rhp_cpu_fixup_sessions", "rhp_expand_records", "rhp_test_chunk_window", "rhp_test_chunk_exact")
 
 _rhp = None
 _host = None

@@ -196,6 +196,22 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
   return 0;
 }
 
+/* test hook: one_chunk_window over the 32 bytes at `line` (tests/test_cpu_units.py
+ * compares it with one_chunk_t); returns 0 when the window cannot decide */
+extern "C" int rhp_test_chunk_window(const uint8_t *line, uint64_t avail, int64_t *res, uint64_t *doff, uint64_t *dlen)
+{
+  uint32_t W[8];
+  memcpy(W, line, 32);
+  return one_chunk_window(W, avail, res, doff, dlen) ? 1 : 0;
+}
+
+/* test hook: one_chunk_t over `body` (size bytes, readable to size + 64) */
+extern "C" int64_t rhp_test_chunk_exact(const uint8_t *body, uint64_t at, uint64_t size, uint64_t *doff, uint64_t *dlen)
+{
+  PlainBytes B{body};
+  return one_chunk_t(B, at, size, doff, dlen);
+}
+
 extern "C" int rhp_expand_records(const rhp_batch_t *b, const rhp_req_t *reqs, const void *hdrs, rhp_hdr_t *out)
 {
   if (!b || !reqs || !out || (b->max_headers && !hdrs)) return -22;

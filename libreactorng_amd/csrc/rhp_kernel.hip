@@ -88,6 +88,7 @@ enum : uint32_t {
    * finalize leaves in http[i] (ret in the low 16 bits) */
   kHintExact = 0x40000000u,
   kHintFrame = 0x80000000u,
+  kHintChunked = 0x20000000u,   /* with kHintFrame: the only candidate is a Transfer-Encoding: chunked */
   /* fr: the first framing candidate's evaluation (late-issue kernel) */
   kFrCarry = 1u,      /* its name is Content-Length, its value is being read (digits in fv) */
   kFrTeName = 2u,     /* its name is Transfer-Encoding, its record not complete yet */
@@ -100,6 +101,7 @@ enum : uint32_t {
   kFrCountSh = 8u,    /* bits 8..15: value bytes read */
   kFrMaxValue = 19u,  /* longer values are left to the replay (19 digits cannot overflow) */
   kFrNeither = 1u << 16,   /* its name, read while its line was open, is neither */
+  kFrChunked = 1u << 17,   /* a Transfer-Encoding whose value is "chunked" (any case) */
   /* workgroup pool area after the staging buffers: counters, then the replay's
    * list; an uneven range's longest-first order (ranges up to kOrderSpan
    * requests) and its histogram live in the staging buffers of the waves such a
@@ -155,7 +157,7 @@ __device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0
  * cycles in the replay's pass 2 (listed scalar paths) / pass 1, 17 requests it
  * ran in pass 2, 18 requests it framed in pass 1, 19 the prologue's loads
  * landed, 20 / 21 late form: decode_window / frame_window cycles (inside
- * section 2).  A section that ends with a wait (`sync`) waits for its LDS reads
+ * section 2), 22 / 23 pass 2's validation and serial paths / staged moves.  A section that ends with a wait (`sync`) waits for its LDS reads
  * (and, where named, its memory) first, so its cycles include their latency.
  * RHP_CLOCK (diagnostic build, tools/kclock.py): shader ticks and 100 MHz
  * ticks from the entry of block 0 wave 0 to its loop's end. */
@@ -168,7 +170,7 @@ __device__ unsigned long long g_clock[2];
 #endif
 struct Diag {
 #ifdef RHP_STAMPS
-  unsigned long long t0 = 0, t1 = 0, c0 = 0, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rp[4] = {0, 0, 0, 0};
+  unsigned long long t0 = 0, t1 = 0, c0 = 0, c1 = 0, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rp[6] = {0, 0, 0, 0, 0, 0};
   unsigned long long rt_entry = 0, rt_loads = 0, rt_loop = 0, n_walk = 0, n_idle = 0, n_idle_live = 0, n_dry = 0;
   __device__ static unsigned long long now()
   {
@@ -219,12 +221,16 @@ struct Diag {
   __device__ void pass_end(uint32_t k) { rp[k] += now() - c0; }   /* 0: pass 2, 1: pass 1 */
   __device__ void framed(bool done) { rp[3] += __popcll(__builtin_amdgcn_ballot_w64(done)); }
   __device__ void slow_path() { rp[2] += __popcll(__builtin_amdgcn_ballot_w64(true)); }
+  /* pass 2's parts: 4 the lanes' validation / serial paths, 5 the wave's staged moves */
+  __device__ void part_begin() { c1 = now(); }
+  __device__ void part_end(uint32_t k) { rp[k] += now() - c1; }
   __device__ void exit(uint32_t waves)
   {
     if ((threadIdx.x & 63u) != 0) return;
     unsigned long long *g = slots(waves);
     g[9] = __builtin_amdgcn_s_memrealtime();
     for (int k = 0; k < 4; k++) g[15 + k] = rp[k];
+    g[22] = rp[4]; g[23] = rp[5];
   }
 #else
   __device__ void entry() {}
@@ -240,6 +246,8 @@ struct Diag {
   __device__ void pass_end(uint32_t) {}
   __device__ void framed(bool) {}
   __device__ void slow_path() {}
+  __device__ void part_begin() {}
+  __device__ void part_end(uint32_t) {}
   __device__ void exit(uint32_t) {}
 #endif
 #ifdef RHP_CLOCK
@@ -523,6 +531,27 @@ __device__ __forceinline__ int http_frame_fast(const uint8_t *b, uint64_t len, i
   return kFrameDone;
 }
 
+/* one_chunk_t for the size line at body offset `at`: the 32 bytes from there in
+ * one round trip (three aligned lines, funnel-shifted to `at`), decided by
+ * one_chunk_window; a line longer than the window goes to one_chunk_t. */
+__device__ __forceinline__ int64_t one_chunk_gpu(const uint8_t *in, uint64_t at, uint64_t size, uint64_t *data_off,
+                                                 uint64_t *data_len, LineBytes &B)
+{
+  typedef __attribute__((address_space(1))) const u32x4 gq;
+  const uintptr_t a = (uintptr_t) (in + at), l = a & ~(uintptr_t) 15;
+  const u32x4 q0 = *reinterpret_cast<gq *>(l), q1 = *reinterpret_cast<gq *>(l + 16), q2 = *reinterpret_cast<gq *>(l + 32);
+  const uint32_t w[12] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], q2[0], q2[1], q2[2], q2[3]};
+  const uint32_t k = (uint32_t) (a >> 2) & 3u, sh = (uint32_t) a & 3u;
+  uint32_t x[9], W[8];
+#pragma unroll
+  for (int m = 0; m < 9; m++) x[m] = k == 0 ? w[m] : k == 1 ? w[m + 1] : k == 2 ? w[m + 2] : w[m + 3];
+#pragma unroll
+  for (int m = 0; m < 8; m++) W[m] = __builtin_amdgcn_alignbyte(x[m + 1], x[m], sh);
+  int64_t res;
+  if (one_chunk_window(W, size - at, &res, data_off, data_len)) return res;
+  return one_chunk_t(B, at, size, data_off, data_len);
+}
+
 /* A chunked body's de-framing (http_dechunk, http.c:134-160).  One thread
  * validates it (the size lines are a dependent walk) and keeps the first
  * kMoveChunks chunks' data spans in registers.  The payload moves -- each
@@ -551,7 +580,7 @@ __device__ __forceinline__ bool frame_chunked(uint8_t *b, uint64_t len, int32_t 
   uint32_t src[kMoveChunks], n[kMoveChunks];   /* kept while the spans stay below 4 GiB (region) */
   int64_t res;
   do {
-    res = one_chunk_t(B, off, size, &doff, &dlen);
+    res = one_chunk_gpu(in, off, size, &doff, &dlen, B);
     if (res <= 0) break;
     if (dlen) {
 #pragma unroll
@@ -572,7 +601,7 @@ __device__ __forceinline__ bool frame_chunked(uint8_t *b, uint64_t len, int32_t 
   o.consumed = (uint64_t) ret + off;
   *x = o;
   if (!compact) return false;
-  if (sb && k <= kMoveChunks && region + 16u <= kStageBody) {
+  if (sb && k <= kMoveChunks && ((uint32_t) (uintptr_t) in & 15u) + region + 20u <= kStageBody) {
     sb->base = (uint64_t) (uintptr_t) in;
     sb->nch = k;
     sb->region = (uint32_t) region;
@@ -604,20 +633,22 @@ __device__ __forceinline__ bool frame_chunked(uint8_t *b, uint64_t len, int32_t 
 }
 
 /* The wave's payload moves for the bodies of the lanes in `m` (their spans in
- * those lanes' *sb), kStageBodies bodies per memory round trip:
+ * those lanes' *sb), kStageBodies bodies per group:
  *  1. the wave loads each body's framed bytes [base & ~15, base + region) as
  *     whole 16-byte lines, 64 lanes side by side (1 KiB per instruction, every
- *     line fetched once), and writes them to the body's LDS slot;
- *  2. lane j then builds the j-th 16-byte block of the de-framed body from LDS
- *     -- for each chunk the block draws on, two aligned ds_read_b128 funnel-
- *     shifted by that chunk's offset and merged by a byte mask -- and stores it:
+ *     line fetched once), and writes them to the body's LDS slot; the next
+ *     group's lines are loaded while this group is built;
+ *  2. lane j builds the j-th aligned 16-byte block of the de-framed body: body
+ *     offset t lies at slot offset lead + t + delta(c), delta(c) = src(c) -
+ *     dst(c) for the chunk c holding t, so the block is five dwords read at the
+ *     lane's own slot address and funnel-shifted (the chunk of its first byte),
+ *     with the bytes from the next chunk's start on taken the same way from
+ *     that chunk (rarely a third: a general pass over the chunks), and stored:
  *     1 KiB of contiguous lines per wave store, only the body's bytes in the
  *     first and last block.
- * Every global load of a round trip lands before its stores (each chunk's
- * data lies at or past its destination, and bodies do not overlap).  The
- * per-thread mover this replaces wrote 16 bytes of 64 different lines per
- * store and fetched each line again once L2 had evicted it (config "chunked":
- * 4.1x the algorithmic bytes, profiles/r03/c/). */
+ * Every global load of a group lands before its stores (each chunk's data lies
+ * at or past its destination, and bodies do not overlap).  Slot reads stay
+ * below lead + region + 20 <= kStageBody (frame_chunked's staging test). */
 __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, uint32_t lane, uint32_t stage)
 {
   typedef __attribute__((address_space(1))) const u32x4 gq;
@@ -625,112 +656,139 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
   typedef __attribute__((address_space(1))) uint8_t gb1;
   typedef __attribute__((address_space(1))) uint32_t gw1;
   typedef __attribute__((address_space(3))) u32x4 lq;
+  typedef __attribute__((address_space(3))) const uint32_t l1;
   constexpr uint32_t kLinesPerLane = kStageBody / 1024u;   /* 16-byte lines per lane per body */
-  while (m) {
-    /* the next kStageBodies bodies: their spans from their lanes (scalar) */
-    uint32_t owner[kStageBodies];
-    bool have[kStageBodies];
+  struct Group {
+    uint32_t owner[kStageBodies];   /* the lane whose body slot q holds (a valid lane for an empty slot) */
+    uint32_t have;                  /* bit q: slot q holds a body */
+  };
+  auto take = [&](Group &g) {
+    g.have = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kStageBodies; q++) {
-      have[q] = m != 0;
-      owner[q] = m ? (uint32_t) __builtin_ctzll(m) : owner[0];
+      g.owner[q] = m ? (uint32_t) __builtin_ctzll(m) : g.owner[0];
+      if (m) g.have |= 1u << q;
       m &= m ? m - 1 : 0ull;
     }
-    uint64_t base[kStageBodies];
-    uint32_t region[kStageBodies];
+  };
+  auto base_of = [&](uint32_t owner) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t) sb.base, owner);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t) (sb.base >> 32), owner);
+    return (uint64_t) lo | (uint64_t) hi << 32;
+  };
+  u32x4 raw[kStageBodies][kLinesPerLane];
+  /* a group's framed lines (lines past a body's region load its first line;
+   * an empty slot loads its group's first body's first line) */
+  auto load = [&](const Group &g) {
 #pragma unroll
     for (uint32_t q = 0; q < kStageBodies; q++) {
-      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t) sb.base, owner[q]);
-      const uint32_t hi = __builtin_amdgcn_readlane((uint32_t) (sb.base >> 32), owner[q]);
-      base[q] = (uint64_t) lo | (uint64_t) hi << 32;
-      region[q] = have[q] ? __builtin_amdgcn_readlane(sb.region, owner[q]) : 0u;
-    }
-    /* 1. framed bytes -> LDS (lines past a body's region load its first line) */
-    u32x4 raw[kStageBodies][kLinesPerLane];
-#pragma unroll
-    for (uint32_t q = 0; q < kStageBodies; q++) {
-      const uint64_t la = base[q] & ~(uint64_t) 15;
-      const uint32_t lines = (uint32_t) ((base[q] + region[q] + 15u - la) >> 4);
+      const uint64_t base = base_of(g.owner[q]);
+      const uint32_t region = (g.have >> q & 1u) ? __builtin_amdgcn_readlane(sb.region, g.owner[q]) : 0u;
+      const uint64_t la = base & ~(uint64_t) 15;
+      const uint32_t lines = (uint32_t) ((base + region + 15u - la) >> 4);
 #pragma unroll
       for (uint32_t h = 0; h < kLinesPerLane; h++) {
         const uint32_t line = lane + 64u * h;
         raw[q][h] = *reinterpret_cast<gq *>((uintptr_t) (la + (line < lines ? 16u * line : 0u)));
       }
     }
+  };
+  /* five slot dwords at the lane's byte position P, funnel-shifted to P */
+  auto fetch = [&](uint32_t slot, uint32_t P) {
+    const l1 *d = reinterpret_cast<const l1 *>((size_t) (slot + (P & ~3u)));
+    const uint32_t w0 = d[0], w1 = d[1], w2 = d[2], w3 = d[3], w4 = d[4], r = P & 3u;
+    return u32x4{__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
+                 __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r)};
+  };
+  /* out's bytes k >= s (0 < s < 16) from o */
+  auto merge_from = [](u32x4 &out, const u32x4 &o, int32_t s) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int32_t c = min(max(s - 4 * j, 0), 4);
+      const uint32_t msk = c >= 4 ? 0u : ~0u << (8 * c);
+      out[j] = (o[j] & msk) | (out[j] & ~msk);
+    }
+  };
+  auto build = [&](uint32_t q, uint32_t owner) {
+    const uint64_t base = base_of(owner);
+    const uint32_t nch = __builtin_amdgcn_readlane(sb.nch, owner);
+    int32_t cd[kMoveChunks + 1], dl[kMoveChunks];   /* body offset of chunk c; its slot shift src - dst (scalar) */
+    cd[0] = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < kMoveChunks; c++) {
+      const uint32_t sp = __builtin_amdgcn_readlane(sb.span[c], owner);
+      dl[c] = (int32_t) (sp & 0xffffu) - cd[c];
+      cd[c + 1] = cd[c] + (int32_t) (sp >> 16);
+    }
+    const int32_t L = cd[kMoveChunks];   /* spans past nch are empty */
+    const uint32_t lead = (uint32_t) base & 15u;
+    const uint64_t a0 = base - lead;
+    const uint32_t blocks = (lead + (uint32_t) L + 15u) >> 4;
+    const uint32_t slot = stage + kStageBody * q;
+    for (uint32_t b = lane; b < blocks; b += 64u) {
+      /* block b: body offsets [t0, t0 + 16); chunk c holds its first byte */
+      const int32_t t0 = (int32_t) (16u * b) - (int32_t) lead;
+      uint32_t c = 0;
+      int32_t d0 = dl[0], d1 = dl[1], e0 = cd[1], e1 = cd[2];
+#pragma unroll
+      for (uint32_t j = 1; j < kMoveChunks; j++) {
+        if (j < nch && cd[j] <= t0) {
+          c = j;
+          d0 = dl[j];
+          e0 = cd[j + 1];
+          d1 = j + 1 < kMoveChunks ? dl[j + 1] : 0;
+          e1 = j + 1 < kMoveChunks ? cd[j + 2] : L;
+        }
+      }
+      u32x4 out = fetch(slot, 16u * b + (uint32_t) d0);
+      bool more = false;
+      if (c + 1 < nch && e0 < t0 + 16) {   /* the next chunk starts inside the block */
+        merge_from(out, fetch(slot, 16u * b + (uint32_t) d1), e0 - t0);
+        more = c + 2 < nch && e1 < t0 + 16;
+      }
+      if (__builtin_amdgcn_ballot_w64(more)) {   /* a chunk of < 16 bytes: every later chunk starting in the block */
+#pragma unroll
+        for (uint32_t j = 2; j < kMoveChunks; j++)
+          if (j < nch && more && j >= c + 2 && cd[j] < t0 + 16)
+            merge_from(out, fetch(slot, 16u * b + (uint32_t) dl[j]), cd[j] - t0);
+      }
+      const uintptr_t A = (uintptr_t) (a0 + 16u * b);
+      if (t0 >= 0 && t0 + 16 <= L) {
+        *reinterpret_cast<gw *>(A) = out;
+      } else {   /* the body's first or last block: only its bytes */
+        const int32_t kb = max(-t0, 0), ke = min(L - t0, 16);
+#pragma unroll
+        for (int32_t j = 0; j < 4; j++) {
+          if (kb <= 4 * j && 4 * j + 4 <= ke) {
+            *reinterpret_cast<gw1 *>(A + 4 * j) = out[j];
+          } else {
+#pragma unroll
+            for (int32_t z = 0; z < 4; z++)
+              if (4 * j + z >= kb && 4 * j + z < ke) *reinterpret_cast<gb1 *>(A + 4 * j + z) = (uint8_t) (out[j] >> (8 * z));
+          }
+        }
+      }
+    }
+  };
+  Group g;
+  take(g);
+  load(g);
+  while (g.have) {
 #pragma unroll
     for (uint32_t q = 0; q < kStageBodies; q++)
 #pragma unroll
       for (uint32_t h = 0; h < kLinesPerLane; h++)
         *reinterpret_cast<lq *>((size_t) (stage + kStageBody * q + 16u * (lane + 64u * h))) = raw[q][h];
     wait_lgkm0();   /* the wave's slots are written (a wave reads its own) */
-    /* 2. the de-framed blocks */
+    Group gn;
+    take(gn);
+    if (gn.have) load(gn);   /* in flight while this group is built */
 #pragma unroll
-    for (uint32_t q = 0; q < kStageBodies; q++) {
-      if (!have[q]) continue;
-      const uint32_t nch = __builtin_amdgcn_readlane(sb.nch, owner[q]);
-      uint32_t cs[kMoveChunks], cn[kMoveChunks], cd[kMoveChunks + 1];   /* span, length, body offset (scalar) */
-      cd[0] = 0;
-#pragma unroll
-      for (uint32_t c = 0; c < kMoveChunks; c++) {
-        const uint32_t sp = __builtin_amdgcn_readlane(sb.span[c], owner[q]);
-        cs[c] = sp & 0xffffu;
-        cn[c] = sp >> 16;
-        cd[c + 1] = cd[c] + cn[c];
-      }
-      const uint32_t L = cd[kMoveChunks];   /* spans past nch are empty */
-      const uint64_t a0 = base[q] & ~(uint64_t) 15;
-      const uint32_t lead = (uint32_t) (base[q] - a0);   /* the body's first byte inside its first line */
-      const uint32_t blocks = (lead + L + 15u) >> 4;
-      for (uint32_t b = lane; b < blocks; b += 64u) {
-        /* block b covers body offsets [t0, t0 + 16), t0 = 16 b - lead */
-        const int32_t t0 = (int32_t) (16u * b) - (int32_t) lead;
-        u32x4 out = u32x4{0, 0, 0, 0};
-        uint32_t keep = 0;
-#pragma unroll
-        for (uint32_t c = 0; c < kMoveChunks; c++) {
-          const int32_t lo_b = (int32_t) cd[c] - t0, hi_b = (int32_t) cd[c + 1] - t0;
-          if (c >= nch || hi_b <= 0 || lo_b >= 16) continue;   /* the block draws nothing from chunk c */
-          /* body byte x of chunk c lies at LDS slot offset lead + cs[c] + (x - cd[c]) */
-          const uint32_t P = (uint32_t) ((int32_t) (lead + cs[c]) + t0 - (int32_t) cd[c]);
-          const uint32_t pl = stage + kStageBody * q + (P & ~15u);
-          const u32x4 l0 = *reinterpret_cast<const lq *>((size_t) pl), l1 = *reinterpret_cast<const lq *>((size_t) pl + 16u);
-          const uint32_t qd = (P >> 2) & 3u, r = P & 3u;
-          const uint32_t w[8] = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
-          const uint32_t lo_c = lo_b < 0 ? 0u : (uint32_t) lo_b, hi_c = hi_b > 16 ? 16u : (uint32_t) hi_b;
-          const uint32_t msk = ((0xffffu >> (16u - (hi_c - lo_c))) << lo_c) & 0xffffu;
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const uint32_t lo = qd == 0 ? w[j] : qd == 1 ? w[j + 1] : qd == 2 ? w[j + 2] : w[j + 3];
-            const uint32_t hi = qd == 0 ? w[j + 1] : qd == 1 ? w[j + 2] : qd == 2 ? w[j + 3] : w[j + 4];
-            const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, r);
-            const uint32_t bm = (msk >> (4 * j)) & 15u;
-            const uint32_t sel = (bm & 1u ? 0xffu : 0u) | (bm & 2u ? 0xff00u : 0u) | (bm & 4u ? 0xff0000u : 0u) |
-                                 (bm & 8u ? 0xff000000u : 0u);
-            out[j] = (v & sel) | (out[j] & ~sel);
-          }
-          keep |= msk;
-        }
-        const uintptr_t A = (uintptr_t) (a0 + 16u * b);
-        if (keep == 0xffffu) {
-          *reinterpret_cast<gw *>(A) = out;
-        } else if (keep) {   /* the body's first or last block: only its bytes */
-#pragma unroll
-          for (uint32_t j = 0; j < 4; j++) {
-            const uint32_t kb = (keep >> (4 * j)) & 15u;
-            if (kb == 15u) {
-              *reinterpret_cast<gw1 *>(A + 4 * j) = out[j];
-            } else if (kb) {
-#pragma unroll
-              for (uint32_t z = 0; z < 4; z++)
-                if (kb >> z & 1u) *reinterpret_cast<gb1 *>(A + 4 * j + z) = (uint8_t) (out[j] >> (8 * z));
-            }
-          }
-        }
-      }
-    }
+    for (uint32_t q = 0; q < kStageBodies; q++)
+      if (g.have >> q & 1u) build(q, g.owner[q]);
+    g = gn;
   }
 }
-
 
 /* Params pointers are generic in the kernel's view (they sit in a struct);
  * the hot stores go through explicit global-address-space pointers so they are
@@ -1243,8 +1301,16 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
           digits = true;
         }
       } else if (nl == 17u && dte == 0) {
-        if (rec_done) fr |= value_len != 0 ? kFrTe : 0u;
-        else fr |= kFrTeName;
+        if (rec_done) {
+          fr |= value_len != 0 ? kFrTe : 0u;
+          /* "chunked" right after ": " (value bytes 19..25 of the line) */
+          const uint32_t value_off = crec_hi & 0xffffu;
+          if (value_len == 7u && value_off == r + 19u && ((d[4] >> 24) | 0x20u) == 'c' &&
+              (d[5] | 0x20202020u) == 0x6b6e7568u && ((d[6] | 0x2020u) & 0xffffu) == 0x6465u)
+            fr |= kFrChunked;
+        } else {
+          fr |= kFrTeName;
+        }
       } else if (!rec_done) {
         fr |= kFrNeither;
       }
@@ -1372,7 +1438,13 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         if (!framed) {
           defer(dcur);
           typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-          *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{cand, kHintFrame | (term_pos + 1u), crec_lo, crec_hi};
+          bool chunked = false;
+          if constexpr (LATE) {
+            const uint32_t hdr = cand & 0x3fffffffu;
+            chunked = !(cand >> 30) && hdr != 0 && (hdr & (hdr - 1)) == 0 && (fr & (kFrChunked | kFrDefer)) == kFrChunked;
+          }
+          *GLOBAL(u32x4a4, &p.http[dcur]) =
+              u32x4a4{cand, kHintFrame | (chunked ? kHintChunked : 0u) | (term_pos + 1u), crec_lo, crec_hi};
         }
       }
     } else if (bad) {
@@ -1779,8 +1851,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       nx = head_at(k + WAVES * 64);
       const uint32_t f = what(cur);
       if (!f) continue;
-      const int fr = (f & kHintExact) ? kFrameSlow
-                                      : http_frame_fast(p.bytes_rw + cur.off, cur.end - cur.off,
+      const int fr = (f & kHintExact)                 ? kFrameSlow
+                     : (cur.hint[1] & kHintChunked) ? kFrameChunked   /* settled in the loop */
+                                                    : http_frame_fast(p.bytes_rw + cur.off, cur.end - cur.off,
                                                         (int32_t) (cur.hint[1] & 0xffffu), &p.http[i], cur.hint[0],
                                                         cur.hint[2], cur.hint[3], p.hdrs + (uint64_t) i * p.hs_req, p.hs_hdr);
       dg.framed(fr == kFrameDone);
@@ -1803,6 +1876,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const uint32_t k = kb + lane;
       StagedBody sb;
       bool staged = false;
+      dg.part_begin();
       if (k < ns) {
         const uint32_t e = slow[k], i = wg_lo + (e & 0x7fffffffu);
         const Head h = head(i);
@@ -1813,9 +1887,12 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
           finish_slow(i, h);
         dg.slow_path();
       }
+      dg.part_end(4);
       if (http) {
         const uint64_t m = __builtin_amdgcn_ballot_w64(staged);
+        dg.part_begin();
         if (m) staged_moves(m, sb, lane, stage);
+        dg.part_end(5);
       }
     }
     dg.pass_end(0);

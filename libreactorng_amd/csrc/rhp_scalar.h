@@ -338,6 +338,62 @@ RHP_HD int64_t one_chunk_t(Bytes &B, uint64_t at, uint64_t size, uint64_t *data_
   return (int64_t) (cs + n + 2);
 }
 
+/* one_chunk_t from a window W of the 32 bytes at `at` (little-endian dwords,
+ * bytes past the buffer's end zero -- the batch is padded), one pass over the
+ * size line as a state machine: the GPU replay loads the window in one memory
+ * round trip where one_chunk_t's line cache takes one per line, and twice when
+ * its LF search crosses a line.  Returns false when the window cannot decide
+ * (no LF in it and more than 32 bytes available); otherwise *res and the data
+ * span are one_chunk_t's. */
+RHP_HD bool one_chunk_window(const uint32_t (&W)[8], uint64_t avail, int64_t *res, uint64_t *data_off,
+                             uint64_t *data_len)
+{
+  enum : uint32_t { kLead, kHex, kTrail, kExt, kCr, kErr };
+  uint32_t st = kLead, nl = 32;
+  bool prev_cr = false, ovf = false;
+  uint64_t cs = 0;
+  for (uint32_t j = 0; j < 32; j++) {
+    const uint32_t c = (W[j >> 2] >> (8 * (j & 3))) & 0xffu;
+    if (c == '\n') {   /* memchr's LF */
+      nl = j;
+      break;
+    }
+    const bool ows = is_ows(c);
+    const uint32_t dg = c - '0', al = (c | 0x20u) - 'a';
+    const bool hex = dg < 10u || al < 6u;
+    if ((st == kLead || st == kHex) && hex) {
+      ovf |= (cs >> 60) != 0;
+      cs = (cs << 4) | (uint64_t) (dg < 10u ? dg : al + 10u);
+      st = kHex;
+    } else if (st == kLead) {
+      st = ows ? kLead : kErr;   /* no digit before this byte: -1 */
+    } else if (st == kHex || st == kTrail) {
+      st = ows ? kTrail : c == ';' ? kExt : c == '\r' ? kCr : kErr;
+    } else if (st == kCr) {
+      st = kErr;                 /* CR not followed by LF */
+    }
+    prev_cr = c == '\r';
+  }
+  if (nl == 32 && avail > 32) return false;
+  if (nl >= avail) {   /* no LF within the body yet */
+    *res = 0;
+    return true;
+  }
+  if (!(st == kCr || (st == kExt && prev_cr)) || ovf || cs == ~0ull) {
+    *res = -1;
+    return true;
+  }
+  const uint64_t n = nl + 1;
+  if (n + 2 > avail || cs > avail - n - 2) {
+    *res = 0;
+    return true;
+  }
+  *data_off = n;
+  *data_len = cs;
+  *res = (int64_t) (cs + n + 2);
+  return true;
+}
+
 /* http_dechunk (http.c:134-160): validate every chunk, then move the payloads
  * down in place, chunk by chunk (dst <= src: the compacted body never passes
  * the next size line).  B reads the body (B(p) = body byte p), move(dst, src, n)

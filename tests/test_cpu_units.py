@@ -186,3 +186,42 @@ def test_emulator_version_errors_vs_oracle(mode, shift):
     emu, _ = rhp.emulate(buf, off, 16, mode)
     want = to_rhp(*run_oracle(buf, off, 16, mode)[:3], mode)
     assert_same(canon(emu, mode), want, buf, off, f"emu version mode{mode} shift{shift}")
+
+
+def test_chunk_window_equals_one_chunk_t():
+    """The GPU replay's windowed size-line parse (rhp_scalar.h one_chunk_window)
+    against the byte-wise one_chunk_t (http.c:73-132) on random size lines:
+    wherever the window decides, the result and the data span are one_chunk_t's,
+    and it decides every line whose LF lies in its 32 bytes (or whose body ends
+    there)."""
+    import ctypes
+    import random
+    h = rhp.host()
+    h.rhp_test_chunk_window.restype = ctypes.c_int
+    h.rhp_test_chunk_exact.restype = ctypes.c_int64
+    alpha = b"0123456789abcdefABCDEF \t;\r\nxgz=\x00" + b"0" * 8 + b"\r\n" * 4
+    rng = random.Random(5)
+    res, doff, dlen = ctypes.c_int64(), ctypes.c_uint64(), ctypes.c_uint64()
+    d2, l2 = ctypes.c_uint64(), ctypes.c_uint64()
+    decided = 0
+    for it in range(60000):
+        kind = it % 4
+        if kind == 0:   # well-formed: OWS? hex OWS? ext? CRLF data CRLF
+            line = (b" " * rng.randrange(3) + f"{rng.randrange(1 << rng.randrange(1, 64)):x}".encode()
+                    + rng.choice([b"", b"\t", b" \t"]) + rng.choice([b"", b";ext=1", b";a\rb"]) + b"\r\n")
+        else:
+            line = bytes(rng.choice(alpha) for _ in range(rng.randrange(0, 40)))
+        body = line + bytes(rng.randrange(256) for _ in range(rng.randrange(0, 64)))
+        size = rng.randrange(0, len(body) + 1) if rng.random() < 0.5 else len(body)
+        buf = (ctypes.c_uint8 * (size + 128))(*body[:size])   # zeros past the body, as the padded batch
+        want = h.rhp_test_chunk_exact(buf, 0, size, ctypes.byref(d2), ctypes.byref(l2))
+        ok = h.rhp_test_chunk_window(buf, size, ctypes.byref(res), ctypes.byref(doff), ctypes.byref(dlen))
+        nl = bytes(buf)[:32].find(b"\n")
+        if (0 <= nl < 32) or size <= 32:
+            assert ok == 1, (line, size)
+        if ok:
+            decided += 1
+            assert res.value == want, (line, size, res.value, want)
+            if want > 0:
+                assert (doff.value, dlen.value) == (d2.value, l2.value), (line, size)
+    assert decided > 50000

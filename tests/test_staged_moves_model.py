@@ -1,14 +1,16 @@
 """A CPU model of rhp_kernel.hip's staged_moves -- the wave's payload moves of
 chunked bodies (http.c:134-160, the memmove of each chunk's data down to the
 running body end): per body the framed bytes as 16-byte lines into an LDS slot,
-then per lane the 16-byte block of the de-framed body built from the slot, one
-funnel-shifted pair of 16-byte slot reads per chunk the block draws on, merged
-by byte masks.  The same arithmetic, lane by lane, over the chunked workload's
-bodies that the kernel stages (<= 8 chunks, framed bytes + 16 <= 2048): the
-blocks rebuild exactly the oracle's de-framed bytes, every global load stays
-inside the body's framed lines, every slot read inside the slot (+ the 32-byte
-overhang the kernel tolerates) and no store leaves the body.  The GPU tests
-check the kernel itself (golden sets and the full-size digest)."""
+then per lane the 16-byte block of the de-framed body: five slot dwords read at
+the lane's own byte position for the chunk holding the block's first byte
+(funnel-shifted), the bytes from the next chunk's start on taken the same way
+from that chunk (and from every later chunk that starts inside the block).  The
+same arithmetic, lane by lane, over the chunked workload's bodies that the
+kernel stages (<= 8 chunks, lead + framed bytes + 20 <= 2048): the blocks
+rebuild exactly the oracle's de-framed bytes, every global load stays inside
+the body's framed lines, every slot read inside the slot and no store leaves
+the body.  The GPU tests check the kernel itself (golden sets and the
+full-size digest)."""
 import numpy as np
 
 import libreactorng_amd as rhp
@@ -35,38 +37,39 @@ def chunk_spans(buf, start, end):
 def staged_body(buf, base, spans, region):
     """one body: returns the (address, byte) stores and checks every access"""
     la = base & ~15
+    lead = base - la
     lines = (base + region + 15 - la) >> 4
     assert lines <= 128
-    slot = bytearray(K_STAGE_BODY + 64)
+    slot = bytearray(K_STAGE_BODY)
     for lane in range(64):
         for h in range(2):
             line = lane + 64 * h
             a = la + (16 * line if line < lines else 0)
             assert la <= a and a + 16 <= la + 16 * max(lines, 1), "a global load outside the body's lines"
             slot[16 * line:16 * line + 16] = bytes(buf[a:a + 16])
-    cd = [0]
-    for _, n in spans:
+    nch = len(spans)
+    cd, dl = [0], []
+    for cs, n in spans:
+        dl.append(cs - cd[-1])
         cd.append(cd[-1] + n)
-    L, lead = cd[-1], base - la
+    L = cd[-1]
+
+    def fetch(P):
+        assert 0 <= P and (P & ~3) + 20 <= K_STAGE_BODY, "a slot read outside the slot"
+        return slot[P:P + 16]
+
     stores = []
     for b in range((lead + L + 15) >> 4):
         t0 = 16 * b - lead
-        out, keep = bytearray(16), [False] * 16
-        for c, (cs, n) in enumerate(spans):
-            lo_b, hi_b = cd[c] - t0, cd[c + 1] - t0
-            if hi_b <= 0 or lo_b >= 16:
-                continue
-            P = lead + cs + t0 - cd[c]
-            assert 0 <= P and (P & ~15) + 32 <= K_STAGE_BODY + 48, "a slot read outside the slot"
-            v = slot[P:P + 16]
-            for k in range(max(lo_b, 0), min(hi_b, 16)):
-                out[k] = v[k]
-                keep[k] = True
+        c = max([j for j in range(nch) if j == 0 or cd[j] <= t0])
+        out = bytearray(fetch(16 * b + dl[c]))
+        for j in range(c + 1, nch):   # every later chunk that starts inside the block, in order
+            if cd[j] < t0 + 16:
+                out[cd[j] - t0:] = fetch(16 * b + dl[j])[cd[j] - t0:]
         A = la + 16 * b
-        for k in range(16):
-            if keep[k]:
-                assert base <= A + k < base + L, "a store outside the body"
-                stores.append((A + k, out[k]))
+        for k in range(max(-t0, 0), min(L - t0, 16)):
+            assert base <= A + k < base + L, "a store outside the body"
+            stores.append((A + k, out[k]))
     return stores
 
 
@@ -82,7 +85,7 @@ def test_staged_moves_model_matches_oracle():
         base, end = int(off[i]) + int(reqs["ret"][i]), int(off[i + 1])
         spans, region = chunk_spans(buf, base, end)
         L = sum(x for _, x in spans)
-        if len(spans) > K_MOVE_CHUNKS or region + 16 > K_STAGE_BODY:
+        if len(spans) > K_MOVE_CHUNKS or (base & 15) + region + 20 > K_STAGE_BODY:
             work[base:base + L] = want[base:base + L]   # the kernel's per-thread mover
             continue
         staged += 1

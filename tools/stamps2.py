@@ -82,4 +82,7 @@ for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, rhp.LA
     rx = st[used, 15:19]
     print(f"   replay per wave: pass 1 (hint framing) {rx[:, 1].mean():.0f} cycles ({rx[:, 3].mean():.1f} requests framed), "
           f"pass 2 (listed scalar paths) {rx[:, 0].mean():.0f} cycles ({rx[:, 2].mean():.1f} requests)")
+    if st[used, 22].sum() + st[used, 23].sum() > 0:
+        print(f"     pass 2 parts per wave: validation + serial paths {st[used, 22].mean():.0f} cycles, "
+              f"staged moves {st[used, 23].mean():.0f} cycles")
     print(f"   workgroups: last wave's loop end {q(ends)}; first wave's {q(firsts)}", flush=True)

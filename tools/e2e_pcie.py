@@ -49,16 +49,29 @@ def _union_ms(spans):
     return tot
 
 
-def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
+def chunk_bounds(n, chunks, taper):
+    """request bounds of the chunks: equal ones, then `taper` chunks of halving size
+    (the last two equal), so the work left after the last H2D -- that chunk's kernel
+    and copies back -- is small"""
+    taper = min(taper, chunks - 1)
+    w = [1.0] * (chunks - taper) + [0.5 ** min(j + 1, taper - 1 if taper > 1 else 1) for j in range(taper)]
+    acc, tot, out = 0.0, sum(w), [0]
+    for x in w[:-1]:
+        acc += x
+        out.append(int(n * acc / tot))
+    return out + [n]
+
+
+def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=3):
     """The end-to-end measurement as a dict (bench.py's `e2e` object)."""
-    args = argparse.Namespace(config=config, n=n, chunks=chunks, streams=streams, reps=reps)
+    args = argparse.Namespace(config=config, n=n, chunks=chunks, streams=streams, reps=reps, taper=taper)
     cfg = CONFIGS[args.config]
     n, maxh, mode = args.n, cfg["maxh"], cfg["mode"]
     buf, off = rhp.generate(cfg["gen"], n, cfg["seed"])
     alg = rhp.header_bytes(cfg["gen"], n, cfg["seed"])
     dev = torch.device("cuda")
     RS = rhp.REQ_DTYPE.itemsize
-    bounds = [n * k // args.chunks for k in range(args.chunks + 1)]
+    bounds = chunk_bounds(n, args.chunks, args.taper)
     # phr mode: compact records (rhp.h RHP_LAYOUT_COMPACT: a 4-byte record per header, header-major in
     # the chunk, the exact path's requests in the chunk's wide area); http mode: header-major rhp_hdr_t
     layout = rhp.LAYOUT_COMPACT if mode == rhp.MODE_PHR else rhp.LAYOUT_HEADER_MAJOR
@@ -118,6 +131,25 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
                 e[3].record(s)
             marks.append(e)
         rows_marks, d2h_bytes = [], RS * n if do_d2h else 0
+        # header rows, on the rows stream: chunk 0's once its request records are on the
+        # host; chunk k+1's speculatively, as many rows as chunks 0..k used, queued behind
+        # its request records (an event wait) when chunk k's are read, so no host round
+        # trip sits between the last kernel and its rows; a chunk that uses more rows than
+        # guessed gets the rest when its records are read
+        guess, spec = 0, {}
+
+        def rows_copy(k, r0, r1):
+            lo, hi = bounds[k], bounds[k + 1]
+            a, b = hbase[k] + r0 * (hi - lo) * HB, hbase[k] + r1 * (hi - lo) * HB
+            e = [EV(), EV()]
+            rows_stream.wait_event(marks[k][3])   # the chunk's kernel has run (its request records copied)
+            with torch.cuda.stream(rows_stream):
+                e[0].record(rows_stream)
+                h_hdrs[a:b].copy_(d_hdrs[a:b], non_blocking=True)
+                e[1].record(rows_stream)
+            rows_marks.append(e)
+            return b - a
+
         for k in range(args.chunks):
             lo, hi = bounds[k], bounds[k + 1]
             if not do_d2h:
@@ -125,22 +157,20 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
             marks[k][3].synchronize()   # chunk k's request records are on the host
             r = reqs_view[lo:hi]
             used = int(r["num_headers"][r["ret"] > 0].max(initial=0))
-            nb = used * (hi - lo) * HB
-            base = hbase[k]
+            have = spec.get(k, 0)
+            if used > have:
+                d2h_bytes += rows_copy(k, have, used)
+            guess = max(guess, used)
+            if k + 1 < args.chunks and guess:
+                spec[k + 1] = guess
+                d2h_bytes += rows_copy(k + 1, 0, guess)
             # compact: requests the exact path parsed keep their records in the chunk's wide area
-            wide = layout == rhp.LAYOUT_COMPACT and bool((r["flags"] & rhp.F_WIDE).any())
-            w0 = base + ((4 * (hi - lo) * maxh + 15) & ~15)
-            wn = (hi - lo) * maxh * rhp.HDR_DTYPE.itemsize if wide else 0
-            e = [EV(), EV()]
-            with torch.cuda.stream(rows_stream):
-                e[0].record(rows_stream)
-                if nb:
-                    h_hdrs[base:base + nb].copy_(d_hdrs[base:base + nb], non_blocking=True)
-                if wn:
+            if layout == rhp.LAYOUT_COMPACT and bool((r["flags"] & rhp.F_WIDE).any()):
+                w0 = hbase[k] + ((4 * (hi - lo) * maxh + 15) & ~15)
+                wn = (hi - lo) * maxh * rhp.HDR_DTYPE.itemsize
+                with torch.cuda.stream(rows_stream):
                     h_hdrs[w0:w0 + wn].copy_(d_hdrs[w0:w0 + wn], non_blocking=True)
-                e[1].record(rows_stream)
-            rows_marks.append(e)
-            d2h_bytes += nb + wn
+                d2h_bytes += wn
         torch.cuda.synchronize()
         if timeline is not None:
             ms = lambda ev: t0.elapsed_time(ev)   # noqa: E731
@@ -188,6 +218,7 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
         "streams": args.streams, "ok_fraction": ok_frac,
         "record_layout": ("compact" if layout == rhp.LAYOUT_COMPACT else "header-major") + " per chunk",
         "parity": parity,
+        "taper": args.taper, "chunk_requests": [bounds[k + 1] - bounds[k] for k in range(args.chunks)],
         "e2e_GiBps": round(alg / t_e2e / gib, 2), "e2e_ms": round(t_e2e * 1e3, 3),
         "kernels_only_GiBps": round(alg / t_kern / gib, 2), "kernels_only_ms": round(t_kern * 1e3, 3),
         "h2d_GBps": round(in_bytes / t_h2d / 1e9, 2), "h2d_ms": round(t_h2d * 1e3, 3),
@@ -196,8 +227,9 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5):
         # the fastest e2e repetition from HIP events: busy time (union of intervals) per engine, and the span
         "timeline_busy_ms": busy, "timeline_span_ms": round(span, 3),
         "timeline_note": "h2d = bytes + offsets per chunk, kernel = rhp_parse_batch per chunk, d2h_reqs = request "
-                         "records, d2h_rows = the header rows the chunk's requests use (issued when its request "
-                         "records have landed)",
+                         "records, d2h_rows = the header rows the chunk's requests use (chunk 0's issued when its "
+                         "request records have landed; chunk k+1's speculatively, as many as chunks 0..k used, "
+                         "behind its request records when chunk k's are read; more rows on a miss)",
     })
 
 
@@ -208,8 +240,9 @@ def main():
     ap.add_argument("--chunks", type=int, default=16)
     ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--taper", type=int, default=3)
     a = ap.parse_args()
-    print(json.dumps(e2e(a.config, a.n, a.chunks, a.streams, a.reps)))
+    print(json.dumps(e2e(a.config, a.n, a.chunks, a.streams, a.reps, a.taper)))
 
 
 if __name__ == "__main__":

@@ -676,10 +676,10 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
     const uint32_t hi = __builtin_amdgcn_readlane((uint32_t) (sb.base >> 32), owner);
     return (uint64_t) lo | (uint64_t) hi << 32;
   };
-  u32x4 raw[kStageBodies][kLinesPerLane];
+  typedef u32x4 Lines[kStageBodies][kLinesPerLane];
   /* a group's framed lines (lines past a body's region load its first line;
    * an empty slot loads its group's first body's first line) */
-  auto load = [&](const Group &g) {
+  auto load = [&](const Group &g, Lines &raw) {
 #pragma unroll
     for (uint32_t q = 0; q < kStageBodies; q++) {
       const uint64_t base = base_of(g.owner[q]);
@@ -770,22 +770,29 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
       }
     }
   };
-  Group g;
-  take(g);
-  load(g);
-  while (g.have) {
+  auto to_slots = [&](const Lines &raw) {
 #pragma unroll
     for (uint32_t q = 0; q < kStageBodies; q++)
 #pragma unroll
       for (uint32_t h = 0; h < kLinesPerLane; h++)
         *reinterpret_cast<lq *>((size_t) (stage + kStageBody * q + 16u * (lane + 64u * h))) = raw[q][h];
     wait_lgkm0();   /* the wave's slots are written (a wave reads its own) */
-    Group gn;
-    take(gn);
-    if (gn.have) load(gn);   /* in flight while this group is built */
+  };
+  auto build_group = [&](const Group &g) {
 #pragma unroll
     for (uint32_t q = 0; q < kStageBodies; q++)
       if (g.have >> q & 1u) build(q, g.owner[q]);
+  };
+  Lines ra;
+  Group g;
+  take(g);
+  load(g, ra);
+  while (g.have) {
+    to_slots(ra);
+    Group gn;
+    take(gn);
+    if (gn.have) load(gn, ra);   /* in flight while this group is built (a second group in flight: slower) */
+    build_group(g);
     g = gn;
   }
 }

@@ -79,10 +79,11 @@ typedef struct rhp_http_req {
 int rhp_http_read_cpu(uint8_t *buf, size_t len, rhp_http_req_t *req, rhp_phr_header_t *fields, size_t *fields_count);
 
 /* Test hooks (tests/test_cpu_units.py): the GPU replay's windowed chunk-size-line
- * parse (rhp_scalar.h one_chunk_window: the 32 bytes at `line`; 0 = undecided)
- * and the byte-wise one it must equal (one_chunk_t, the size line at body
- * offset `at`; the body readable to size + 64). */
-int rhp_test_chunk_window(const uint8_t *line, uint64_t avail, int64_t *res, uint64_t *data_off, uint64_t *data_len);
+ * parse (rhp_scalar.h one_chunk_window: the nw <= 32 bytes at `line`, 32
+ * readable; 0 = undecided) and the byte-wise one it must equal (one_chunk_t,
+ * the size line at body offset `at`; the body readable to size + 64). */
+int rhp_test_chunk_window(const uint8_t *line, uint32_t nw, uint64_t avail, int64_t *res, uint64_t *data_off,
+                          uint64_t *data_len);
 int64_t rhp_test_chunk_exact(const uint8_t *body, uint64_t at, uint64_t size, uint64_t *data_off, uint64_t *data_len);
 
 #ifdef __cplusplus

@@ -196,13 +196,15 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
   return 0;
 }
 
-/* test hook: one_chunk_window over the 32 bytes at `line` (tests/test_cpu_units.py
- * compares it with one_chunk_t); returns 0 when the window cannot decide */
-extern "C" int rhp_test_chunk_window(const uint8_t *line, uint64_t avail, int64_t *res, uint64_t *doff, uint64_t *dlen)
+/* test hook: one_chunk_window over the nw (<= 32) bytes at `line`
+ * (tests/test_cpu_units.py compares it with one_chunk_t); returns 0 when the
+ * window cannot decide */
+extern "C" int rhp_test_chunk_window(const uint8_t *line, uint32_t nw, uint64_t avail, int64_t *res, uint64_t *doff,
+                                     uint64_t *dlen)
 {
   uint32_t W[8];
   memcpy(W, line, 32);
-  return one_chunk_window(W, avail, res, doff, dlen) ? 1 : 0;
+  return one_chunk_window(W, nw, avail, res, doff, dlen) ? 1 : 0;
 }
 
 /* test hook: one_chunk_t over `body` (size bytes, readable to size + 64) */

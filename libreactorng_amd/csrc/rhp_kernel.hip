@@ -531,105 +531,146 @@ __device__ __forceinline__ int http_frame_fast(const uint8_t *b, uint64_t len, i
   return kFrameDone;
 }
 
-/* one_chunk_t for the size line at body offset `at`: the 32 bytes from there in
- * one round trip (three aligned lines, funnel-shifted to `at`), decided by
- * one_chunk_window; a line longer than the window goes to one_chunk_t. */
-__device__ __forceinline__ int64_t one_chunk_gpu(const uint8_t *in, uint64_t at, uint64_t size, uint64_t *data_off,
-                                                 uint64_t *data_len, LineBytes &B)
-{
-  typedef __attribute__((address_space(1))) const u32x4 gq;
-  const uintptr_t a = (uintptr_t) (in + at), l = a & ~(uintptr_t) 15;
-  const u32x4 q0 = *reinterpret_cast<gq *>(l), q1 = *reinterpret_cast<gq *>(l + 16), q2 = *reinterpret_cast<gq *>(l + 32);
-  const uint32_t w[12] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], q2[0], q2[1], q2[2], q2[3]};
-  const uint32_t k = (uint32_t) (a >> 2) & 3u, sh = (uint32_t) a & 3u;
-  uint32_t x[9], W[8];
-#pragma unroll
-  for (int m = 0; m < 9; m++) x[m] = k == 0 ? w[m] : k == 1 ? w[m + 1] : k == 2 ? w[m + 2] : w[m + 3];
-#pragma unroll
-  for (int m = 0; m < 8; m++) W[m] = __builtin_amdgcn_alignbyte(x[m + 1], x[m], sh);
-  int64_t res;
-  if (one_chunk_window(W, size - at, &res, data_off, data_len)) return res;
-  return one_chunk_t(B, at, size, data_off, data_len);
-}
-
-/* A chunked body's de-framing (http_dechunk, http.c:134-160).  One thread
- * validates it (the size lines are a dependent walk) and keeps the first
- * kMoveChunks chunks' data spans in registers.  The payload moves -- each
- * chunk's data down to the running body end, in order -- then go one of two
- * ways:
- *  - staged by the wave (staged_moves, below), when the body has at most
- *    kMoveChunks chunks and its framed bytes fit a kStageBody slot: the
- *    function leaves the spans in *sb and returns true;
- *  - by this thread (DevMove from the kept spans, or from a second walk of
- *    the size lines for a body of more chunks), returning false. */
 enum : uint32_t { kMoveChunks = 8, kStageBody = 2048, kStageBodies = 4 };
-struct StagedBody {
-  uint64_t base;           /* the body's first byte: the de-framed body goes to [base, base + len) */
-  uint32_t nch, region;    /* data chunks; framed bytes up to the last data byte */
-  uint32_t span[kMoveChunks];   /* chunk c's data: [base + (span & 0xffff), + (span >> 16)) (< kStageBody) */
-};
-__device__ __forceinline__ bool frame_chunked(uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x, bool compact,
-                                              StagedBody *sb = nullptr)
-{
-  rhp_http_t o = {1, compact ? 1u : (uint32_t) RHP_BODY_CHUNKED_PENDING, 0, 0};
-  uint8_t *in = b + ret;
-  const uint64_t size = len - (uint64_t) ret;
-  LineBytes B{in, ~0ull, {0, 0, 0, 0}};
-  uint64_t off = 0, doff = 0, dlen = 0, sum = 0, region = 0;
-  uint32_t k = 0;
-  uint32_t src[kMoveChunks], n[kMoveChunks];   /* kept while the spans stay below 4 GiB (region) */
-  int64_t res;
-  do {
-    res = one_chunk_gpu(in, off, size, &doff, &dlen, B);
-    if (res <= 0) break;
-    if (dlen) {
+
+/* A chunked body's validation (http_dechunk's first pass, http.c:134-150) as
+ * a walk one size line per step: a step parses the 17-20 bytes from the line's
+ * start (one_chunk_window; a longer line goes to one_chunk_t) in the two
+ * aligned lines the previous step loaded, and loads the next line's.  The walk keeps
+ * the first kMoveChunks chunks' data spans.  One step per memory round trip:
+ * the replay runs the next round's walks inside this round's payload moves
+ * (staged_moves), one step per body group, so the walk's chain of round trips
+ * hides behind the moves. */
+struct ChunkWalk {
+  uint8_t *in;          /* the body's first byte */
+  uint64_t size, off;   /* bytes of the body; the next size line's offset */
+  uint64_t sum, region; /* data bytes; framed bytes up to the last data byte */
+  int32_t res;          /* when done: 1 valid, 0 need more, -1 malformed */
+  uint32_t k;           /* data chunks */
+  uint32_t span[kMoveChunks];   /* chunk c's data: (off | len << 16) from `in` (exact while region <= 0xffff) */
+  bool live;
+  u32x4 q[2];           /* the two aligned lines from the next size line's start, loading */
+  __device__ __forceinline__ void issue()
+  {
+    typedef __attribute__((address_space(1))) const u32x4 gq;
+    const uintptr_t l = (uintptr_t) (in + off) & ~(uintptr_t) 15;
 #pragma unroll
-      for (uint32_t j = 0; j < kMoveChunks; j++)
-        if (j == k) { src[j] = (uint32_t) (off + doff); n[j] = (uint32_t) dlen; }
+    for (int j = 0; j < 2; j++) q[j] = *reinterpret_cast<gq *>(l + 16 * j);
+  }
+  __device__ __forceinline__ void begin(uint8_t *body, uint64_t n)
+  {
+    in = body; size = n; off = sum = region = 0; res = 0; k = 0; live = true;
+    issue();
+  }
+  __device__ __forceinline__ void step()
+  {
+    if (!live) return;
+    const uintptr_t a = (uintptr_t) (in + off);
+    const uint32_t w[9] = {q[0][0], q[0][1], q[0][2], q[0][3], q[1][0], q[1][1], q[1][2], q[1][3], 0u};
+    const uint32_t qd = (uint32_t) (a >> 2) & 3u, sh = (uint32_t) a & 3u;
+    uint32_t x[6], W[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int m = 0; m < 6; m++) x[m] = qd == 0 ? w[m] : qd == 1 ? w[m + 1] : qd == 2 ? w[m + 2] : w[m + 3];
+#pragma unroll
+    for (int m = 0; m < 5; m++) W[m] = __builtin_amdgcn_alignbyte(x[m + 1], x[m], sh);
+    int64_t r;
+    uint64_t doff = 0, dlen = 0;
+    /* W holds 20 bytes from the line's start, of them 32 - (a & 15) >= 17 in the two lines */
+    if (!one_chunk_window(W, min(20u, 32u - ((uint32_t) a & 15u)), size - off, &r, &doff, &dlen)) {
+      LineBytes B{in, ~0ull, {0, 0, 0, 0}};
+      r = one_chunk_t(B, off, size, &doff, &dlen);
+    }
+    if (r <= 0) {
+      res = (int32_t) r;
+      live = false;
+      return;
+    }
+    if (dlen) {
+      const uint32_t sp = (uint32_t) (off + doff) | (uint32_t) dlen << 16;
+#pragma unroll
+      for (uint32_t j = 0; j < kMoveChunks; j++) span[j] = j == k ? sp : span[j];   /* every element stored: no indexed store */
       k++;
       region = off + doff + dlen;
     }
-    off += (uint64_t) res;
+    off += (uint64_t) r;
     sum += dlen;
-  } while (dlen);
-  if (res <= 0) {
-    o.result = (int32_t) res;
+    if (!dlen) {   /* the last chunk */
+      res = 1;
+      live = false;
+      return;
+    }
+    issue();
+  }
+};
+
+/* The body's record and payload moves once its walk is done (http.c:150-160).
+ * The moves -- each chunk's data down to the running body end, in order --
+ * go one of two ways:
+ *  - staged by the wave (staged_moves, below), when the body has at most
+ *    kMoveChunks chunks and its framed bytes fit a kStageBody slot: the spans
+ *    go to *sb and the function returns true;
+ *  - by this thread (DevMove from the kept spans, or from a second walk of
+ *    the size lines for a body of more chunks or beyond 64 KiB), returning
+ *    false. */
+struct StagedBody {
+  uint64_t base;           /* the body's first byte: the de-framed body goes to [base, base + len) */
+  uint32_t nch, region;    /* data chunks; framed bytes up to the last data byte */
+  uint32_t size;           /* the body's bytes up to the request's end (capped at 2 * kStageBody) */
+  uint32_t span[kMoveChunks];   /* chunk c's data: [base + (span & 0xffff), + (span >> 16)) (< kStageBody) */
+};
+__device__ __forceinline__ bool finish_chunked(const ChunkWalk &w, int32_t ret, rhp_http_t *x, bool compact,
+                                               StagedBody *sb)
+{
+  rhp_http_t o = {1, compact ? 1u : (uint32_t) RHP_BODY_CHUNKED_PENDING, 0, 0};
+  if (w.res <= 0) {
+    o.result = (int32_t) w.res;
     *x = o;
     return false;
   }
-  o.body_len = sum;
-  o.consumed = (uint64_t) ret + off;
+  o.body_len = w.sum;
+  o.consumed = (uint64_t) ret + w.off;
   *x = o;
   if (!compact) return false;
-  if (sb && k <= kMoveChunks && ((uint32_t) (uintptr_t) in & 15u) + region + 20u <= kStageBody) {
-    sb->base = (uint64_t) (uintptr_t) in;
-    sb->nch = k;
-    sb->region = (uint32_t) region;
+  if (sb && w.k <= kMoveChunks && ((uint32_t) (uintptr_t) w.in & 15u) + w.region + 20u <= kStageBody) {
+    sb->base = (uint64_t) (uintptr_t) w.in;
+    sb->nch = w.k;
+    sb->region = (uint32_t) w.region;
+    sb->size = (uint32_t) min(w.size, (uint64_t) (2 * kStageBody));
 #pragma unroll
-    for (uint32_t j = 0; j < kMoveChunks; j++) sb->span[j] = j < k ? (uint32_t) src[j] | (uint32_t) n[j] << 16 : 0u;
+    for (uint32_t j = 0; j < kMoveChunks; j++) sb->span[j] = j < w.k ? w.span[j] : 0u;
     return true;
   }
-  DevMove M{in};
-  if (k <= kMoveChunks && region <= 0xffffffffull) {
-    uint64_t total = 0;
+  DevMove M{w.in};
+  uint64_t total = 0;
+  if (w.k <= kMoveChunks && w.region <= 0xffffu) {
 #pragma unroll
     for (uint32_t j = 0; j < kMoveChunks; j++) {
-      if (j < k) {
-        M(total, src[j], n[j]);
-        total += n[j];
+      if (j < w.k) {
+        M(total, w.span[j] & 0xffffu, w.span[j] >> 16);
+        total += w.span[j] >> 16;
       }
     }
     return false;
   }
-  uint64_t total = 0;
-  off = 0;
+  LineBytes B{w.in, ~0ull, {0, 0, 0, 0}};
+  uint64_t off = 0, doff = 0, dlen = 0;
   do {
-    res = one_chunk_t(B, off, size, &doff, &dlen);
+    const int64_t res = one_chunk_t(B, off, w.size, &doff, &dlen);
     M(total, off + doff, dlen);
     off += (uint64_t) res;
     total += dlen;
   } while (dlen);
   return false;
+}
+
+/* a chunked body walked and finished by this thread alone */
+__device__ __forceinline__ bool frame_chunked(uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x, bool compact,
+                                              StagedBody *sb = nullptr)
+{
+  ChunkWalk w;
+  w.begin(b + ret, len - (uint64_t) ret);
+  while (w.live) w.step();
+  return finish_chunked(w, ret, x, compact, sb);
 }
 
 /* The wave's payload moves for the bodies of the lanes in `m` (their spans in
@@ -649,7 +690,8 @@ __device__ __forceinline__ bool frame_chunked(uint8_t *b, uint64_t len, int32_t 
  * Every global load of a group lands before its stores (each chunk's data lies
  * at or past its destination, and bodies do not overlap).  Slot reads stay
  * below lead + region + 20 <= kStageBody (frame_chunked's staging test). */
-__device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, uint32_t lane, uint32_t stage)
+template <class Step>
+__device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, uint32_t lane, uint32_t stage, Step &&step)
 {
   typedef __attribute__((address_space(1))) const u32x4 gq;
   typedef __attribute__((address_space(1))) u32x4 gw;
@@ -721,6 +763,7 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
       cd[c + 1] = cd[c] + (int32_t) (sp >> 16);
     }
     const int32_t L = cd[kMoveChunks];   /* spans past nch are empty */
+    const int32_t size = (int32_t) __builtin_amdgcn_readlane(sb.size, owner);
     const uint32_t lead = (uint32_t) base & 15u;
     const uint64_t a0 = base - lead;
     const uint32_t blocks = (lead + (uint32_t) L + 15u) >> 4;
@@ -748,14 +791,34 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
       }
       if (__builtin_amdgcn_ballot_w64(more)) {   /* a chunk of < 16 bytes: every later chunk starting in the block */
 #pragma unroll
-        for (uint32_t j = 2; j < kMoveChunks; j++)
-          if (j < nch && more && j >= c + 2 && cd[j] < t0 + 16)
+        for (uint32_t j = 2; j < kMoveChunks; j++) {
+          const bool take_j = j < nch && more && j >= c + 2 && cd[j] < t0 + 16;
+          if (__builtin_amdgcn_ballot_w64(take_j) && take_j)
             merge_from(out, fetch(slot, 16u * b + (uint32_t) dl[j]), cd[j] - t0);
+        }
       }
       const uintptr_t A = (uintptr_t) (a0 + 16u * b);
-      if (t0 >= 0 && t0 + 16 <= L) {
+      /* the body's first and last block keep the bytes around the body: the
+       * slot holds this line as it is in memory, and where the line lies in
+       * the request (its header bytes before the body, its framing after) the
+       * whole line is stored, those bytes unchanged; a line reaching into the
+       * next request is written byte by byte (the caller may be filling that
+       * request while this one parses) */
+      const bool inner = t0 >= 0 && t0 + 16 <= L;
+      const bool whole = inner || t0 + 16 <= size;
+      if (!inner && whole) {
+        const u32x4 orig = *reinterpret_cast<const lq *>((size_t) (slot + 16u * b));
+        const int32_t kb = max(-t0, 0), ke = min(L - t0, 16);
+#pragma unroll
+        for (int32_t j = 0; j < 4; j++) {
+          const int32_t lo = min(max(kb - 4 * j, 0), 4), hi = min(max(ke - 4 * j, 0), 4);
+          const uint32_t msk = hi > lo ? (~0u >> (32 - 8 * (hi - lo))) << (8 * lo) : 0u;
+          out[j] = (out[j] & msk) | (orig[j] & ~msk);
+        }
+      }
+      if (whole) {
         *reinterpret_cast<gw *>(A) = out;
-      } else {   /* the body's first or last block: only its bytes */
+      } else {   /* only the body's bytes */
         const int32_t kb = max(-t0, 0), ke = min(L - t0, 16);
 #pragma unroll
         for (int32_t j = 0; j < 4; j++) {
@@ -789,6 +852,7 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
   load(g, ra);
   while (g.have) {
     to_slots(ra);
+    step();   /* the caller's per-group work (the next round's walks): its loads go out before the next group's */
     Group gn;
     take(gn);
     if (gn.have) load(gn, ra);   /* in flight while this group is built (a second group in flight: slower) */
@@ -1877,29 +1941,51 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     __syncthreads();
     dg.pass_begin();
     const uint32_t ns = min(*slow_n, kSlowCap);
-    /* wave-uniform trips: the chunked bodies its lanes validated are moved by
-     * the whole wave (staged_moves) */
-    for (uint32_t kb = tid & ~63u; kb < ns; kb += WAVES * 64) {
+    /* wave-uniform rounds of 64 entries: the chunked bodies the lanes walked
+     * are moved by the whole wave (staged_moves), and the next round's walks
+     * step inside those moves */
+    ChunkWalk w;
+    w.live = false;
+    uint32_t wi = 0;
+    int32_t wret = 0;
+    bool walking = false;
+    auto start_round = [&](uint32_t kb) {
       const uint32_t k = kb + lane;
-      StagedBody sb;
-      bool staged = false;
+      walking = false;
+      w.live = false;
       dg.part_begin();
       if (k < ns) {
         const uint32_t e = slow[k], i = wg_lo + (e & 0x7fffffffu);
         const Head h = head(i);
-        if (http && (e >> 31))   /* chunked bodies: http mode only */
-          staged = frame_chunked(p.bytes_rw + h.off, h.end - h.off, (int32_t) (h.hint[1] & 0xffffu), &p.http[i],
-                                 p.compact, &sb);
-        else
+        if (http && (e >> 31)) {   /* chunked bodies: http mode only */
+          wi = i;
+          wret = (int32_t) (h.hint[1] & 0xffffu);
+          w.begin(p.bytes_rw + h.off + (uint32_t) wret, (h.end - h.off) - (uint64_t) wret);
+          walking = true;
+        } else {
           finish_slow(i, h);
+        }
         dg.slow_path();
       }
       dg.part_end(4);
-      if (http) {
-        const uint64_t m = __builtin_amdgcn_ballot_w64(staged);
+    };
+    uint32_t kb = tid & ~63u;
+    if (kb < ns) start_round(kb);
+    for (; kb < ns; kb += WAVES * 64) {
+      if constexpr (http) {
         dg.part_begin();
-        if (m) staged_moves(m, sb, lane, stage);
+        while (__builtin_amdgcn_ballot_w64(w.live)) w.step();   /* what the last round's moves left */
+        StagedBody sb;
+        const bool staged = walking && finish_chunked(w, wret, &p.http[wi], p.compact, &sb);
+        dg.part_end(4);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(staged);
+        if (kb + WAVES * 64 < ns) start_round(kb + WAVES * 64);
+        else walking = w.live = false;
+        dg.part_begin();
+        if (m) staged_moves(m, sb, lane, stage, [&]() { w.step(); });
         dg.part_end(5);
+      } else {
+        if (kb + WAVES * 64 < ns) start_round(kb + WAVES * 64);
       }
     }
     dg.pass_end(0);

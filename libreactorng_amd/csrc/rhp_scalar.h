@@ -338,14 +338,14 @@ RHP_HD int64_t one_chunk_t(Bytes &B, uint64_t at, uint64_t size, uint64_t *data_
   return (int64_t) (cs + n + 2);
 }
 
-/* one_chunk_t from a window W of the 32 bytes at `at` (little-endian dwords,
- * bytes past the buffer's end zero -- the batch is padded), one pass over the
- * size line as a state machine: the GPU replay loads the window in one memory
- * round trip where one_chunk_t's line cache takes one per line, and twice when
- * its LF search crosses a line.  Returns false when the window cannot decide
- * (no LF in it and more than 32 bytes available); otherwise *res and the data
- * span are one_chunk_t's. */
-RHP_HD bool one_chunk_window(const uint32_t (&W)[8], uint64_t avail, int64_t *res, uint64_t *data_off,
+/* one_chunk_t from a window W holding the `nw` (<= 32) bytes at `at` (little-
+ * endian dwords; bytes past the buffer's end zero -- the batch is padded), one
+ * pass over the size line as a state machine: the GPU replay loads the window
+ * in one memory round trip where one_chunk_t's line cache takes one per line,
+ * and twice when its LF search crosses a line.  Returns false when the window
+ * cannot decide (no LF in it and more than nw bytes available); otherwise *res
+ * and the data span are one_chunk_t's. */
+RHP_HD bool one_chunk_window(const uint32_t (&W)[8], uint32_t nw, uint64_t avail, int64_t *res, uint64_t *data_off,
                              uint64_t *data_len)
 {
   enum : uint32_t { kLead, kHex, kTrail, kExt, kCr, kErr };
@@ -353,6 +353,7 @@ RHP_HD bool one_chunk_window(const uint32_t (&W)[8], uint64_t avail, int64_t *re
   bool prev_cr = false, ovf = false;
   uint64_t cs = 0;
   for (uint32_t j = 0; j < 32; j++) {
+    if (j >= nw) break;
     const uint32_t c = (W[j >> 2] >> (8 * (j & 3))) & 0xffu;
     if (c == '\n') {   /* memchr's LF */
       nl = j;
@@ -374,7 +375,7 @@ RHP_HD bool one_chunk_window(const uint32_t (&W)[8], uint64_t avail, int64_t *re
     }
     prev_cr = c == '\r';
   }
-  if (nl == 32 && avail > 32) return false;
+  if (nl == 32 && avail > nw) return false;
   if (nl >= avail) {   /* no LF within the body yet */
     *res = 0;
     return true;

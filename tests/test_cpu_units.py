@@ -192,12 +192,13 @@ def test_chunk_window_equals_one_chunk_t():
     """The GPU replay's windowed size-line parse (rhp_scalar.h one_chunk_window)
     against the byte-wise one_chunk_t (http.c:73-132) on random size lines:
     wherever the window decides, the result and the data span are one_chunk_t's,
-    and it decides every line whose LF lies in its 32 bytes (or whose body ends
-    there)."""
+    and it decides every line whose LF lies in its 17-32 bytes (or whose body
+    ends there); the bytes past the window are garbage it must not read."""
     import ctypes
     import random
     h = rhp.host()
     h.rhp_test_chunk_window.restype = ctypes.c_int
+    h.rhp_test_chunk_window.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64] + [ctypes.c_void_p] * 3
     h.rhp_test_chunk_exact.restype = ctypes.c_int64
     alpha = b"0123456789abcdefABCDEF \t;\r\nxgz=\x00" + b"0" * 8 + b"\r\n" * 4
     rng = random.Random(5)
@@ -215,10 +216,12 @@ def test_chunk_window_equals_one_chunk_t():
         size = rng.randrange(0, len(body) + 1) if rng.random() < 0.5 else len(body)
         buf = (ctypes.c_uint8 * (size + 128))(*body[:size])   # zeros past the body, as the padded batch
         want = h.rhp_test_chunk_exact(buf, 0, size, ctypes.byref(d2), ctypes.byref(l2))
-        ok = h.rhp_test_chunk_window(buf, size, ctypes.byref(res), ctypes.byref(doff), ctypes.byref(dlen))
-        nl = bytes(buf)[:32].find(b"\n")
-        if (0 <= nl < 32) or size <= 32:
-            assert ok == 1, (line, size)
+        nw = 32 if it % 2 else rng.randrange(17, 33)   # the kernel's two lines hold 17..32 bytes from the line
+        win = (ctypes.c_uint8 * 32)(*(bytes(buf)[:nw] + bytes(rng.randrange(256) for _ in range(32 - nw))))
+        ok = h.rhp_test_chunk_window(win, nw, size, ctypes.byref(res), ctypes.byref(doff), ctypes.byref(dlen))
+        nl = bytes(buf)[:nw].find(b"\n")
+        if nl >= 0 or size <= nw:
+            assert ok == 1, (line, size, nw)
         if ok:
             decided += 1
             assert res.value == want, (line, size, res.value, want)

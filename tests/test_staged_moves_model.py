@@ -8,8 +8,9 @@ from that chunk (and from every later chunk that starts inside the block).  The
 same arithmetic, lane by lane, over the chunked workload's bodies that the
 kernel stages (<= 8 chunks, lead + framed bytes + 20 <= 2048): the blocks
 rebuild exactly the oracle's de-framed bytes, every global load stays inside
-the body's framed lines, every slot read inside the slot and no store leaves
-the body.  The GPU tests check the kernel itself (golden sets and the
+the body's framed lines, every slot read inside the slot, and a store leaves
+the body only as a whole line inside the request that rewrites the bytes
+around the body with their own values.  The GPU tests check the kernel itself (golden sets and the
 full-size digest)."""
 import numpy as np
 
@@ -34,7 +35,7 @@ def chunk_spans(buf, start, end):
         at = data + size + 2
 
 
-def staged_body(buf, base, spans, region):
+def staged_body(buf, base, spans, region, size, req_start):
     """one body: returns the (address, byte) stores and checks every access"""
     la = base & ~15
     lead = base - la
@@ -67,9 +68,20 @@ def staged_body(buf, base, spans, region):
             if cd[j] < t0 + 16:
                 out[cd[j] - t0:] = fetch(16 * b + dl[j])[cd[j] - t0:]
         A = la + 16 * b
-        for k in range(max(-t0, 0), min(L - t0, 16)):
-            assert base <= A + k < base + L, "a store outside the body"
-            stores.append((A + k, out[k]))
+        kb, ke = max(-t0, 0), min(L - t0, 16)
+        if (0 <= t0 and t0 + 16 <= L) or t0 + 16 <= size:
+            # a whole line: the bytes outside the body from the slot (the line as it is in memory),
+            # all of them inside this request
+            for k in range(16):
+                v = out[k] if kb <= k < ke else slot[16 * b + k]
+                assert req_start <= A + k < base + size, "a whole-line store outside the request"
+                if not kb <= k < ke:
+                    assert v == buf[A + k], "a byte around the body changed"
+                stores.append((A + k, v))
+        else:
+            for k in range(kb, ke):
+                assert base <= A + k < base + L, "a store outside the body"
+                stores.append((A + k, out[k]))
     return stores
 
 
@@ -89,7 +101,7 @@ def test_staged_moves_model_matches_oracle():
             work[base:base + L] = want[base:base + L]   # the kernel's per-thread mover
             continue
         staged += 1
-        for a, v in staged_body(buf, base, spans, region):   # every load before any store (one body)
+        for a, v in staged_body(buf, base, spans, region, end - base, int(off[i])):   # every load before any store
             work[a] = v
     assert staged > n * 0.8
     assert np.array_equal(work, want), f"{int((work != want).sum())} bytes differ from the oracle's"

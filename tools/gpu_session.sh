@@ -21,7 +21,7 @@ step_bench() {
 step_prof() {
   for c in get256 zipf post chunked; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_${TAG}_$c -o run \
-      -- python3 bench.py --config $c --extra none --steps 30 --warmup 5 --no-cpu --no-e2e > gpurun_out/prof_${TAG}_$c.log 2>&1 \
+      -- python3 bench.py --config $c --extra none --steps 30 --warmup 5 --streams 1 --no-cpu --no-e2e > gpurun_out/prof_${TAG}_$c.log 2>&1 \
       || return 1
     echo PROF_${c}_OK
   done

@@ -2,7 +2,9 @@
 ends in host memory -- the io_uring recv buffer").
 
 The batch (config 2 by default: 1M x 256 B) sits in pinned host memory; it is cut
-into chunks that stream through S HIP streams: pinned hipMemcpyAsync H2D of the
+into chunks that stream through S HIP streams (chunk k on stream k mod S; one
+stream per engine -- H2D, kernels, D2H -- measured slower: 34-38 GiB/s, the copies
+back trailing the last H2D by 0.8-1.8 ms): pinned hipMemcpyAsync H2D of the
 chunk's bytes and offsets -> rhp_parse_batch on that chunk (header records
 header-major within the chunk: compact 4-byte records in phr mode, rhp.h) -> D2H
 of the chunk's request records.  The host reads each chunk's request records as
@@ -23,6 +25,7 @@ says which engine was busy (or idle) for how long.
 usage: python tools/e2e_pcie.py [--config get256] [--chunks 16] [--streams 3] [--reps 5]
 """
 import argparse
+import gc
 import ctypes
 import json
 import os
@@ -187,9 +190,14 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0):
         best, best_tl, nbytes = None, None, 0
         for _ in range(args.reps):
             ev = {}
-            t0 = time.perf_counter()
-            nbytes = run(timeline=ev, **kw)
-            t = time.perf_counter() - t0
+            gc.collect()
+            gc.disable()   # a collection inside the enqueue loop leaves the copy engine idle
+            try:
+                t0 = time.perf_counter()
+                nbytes = run(timeline=ev, **kw)
+                t = time.perf_counter() - t0
+            finally:
+                gc.enable()
             if best is None or t < best:
                 best, best_tl = t, timeline_of(ev)
         return best, best_tl, nbytes
@@ -216,6 +224,11 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0):
     gib = 2 ** 30
     busy = {k: round(_union_ms(v), 3) for k, v in tl.items()}
     span = max(b for v in tl.values() for _, b in v) if tl else 0.0
+    h2d = sorted(tl.get("h2d", []))
+    # where the span goes besides H2D: before the first copy, idle gaps between copies, after the last one
+    h2d_edges = {"before_first_h2d_ms": round(h2d[0][0], 3) if h2d else 0.0,
+                 "h2d_idle_gaps_ms": round(sum(max(0.0, b[0] - a[1]) for a, b in zip(h2d, h2d[1:])), 3),
+                 "after_last_h2d_ms": round(span - h2d[-1][1], 3) if h2d else 0.0}
     return ({
         "config": args.config, "requests": n, "algorithmic_bytes": int(alg), "chunks": args.chunks,
         "streams": args.streams, "ok_fraction": ok_frac,
@@ -228,7 +241,7 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0):
         "h2d_bytes": int(in_bytes), "d2h_bytes": int(d2h_bytes),
         "d2h_bytes_per_request": round(d2h_bytes / n, 2),
         # the fastest e2e repetition from HIP events: busy time (union of intervals) per engine, and the span
-        "timeline_busy_ms": busy, "timeline_span_ms": round(span, 3),
+        "timeline_busy_ms": busy, "timeline_span_ms": round(span, 3), "timeline_h2d_edges": h2d_edges,
         "timeline_note": "h2d = bytes + offsets per chunk, kernel = rhp_parse_batch per chunk, d2h_reqs = request "
                          "records, d2h_rows = the header rows the chunk's requests use (chunk 0's issued when its "
                          "request records have landed; chunk k+1's speculatively, as many as chunks 0..k used, "

@@ -117,7 +117,10 @@ typedef struct rhp_http {
 typedef struct rhp_batch {
   const uint8_t  *bytes;   /* device, 16-byte aligned: packed requests + RHP_PAD zero bytes */
   uint8_t        *bytes_rw;/* device, RHP_MODE_HTTP: same buffer, writable (chunked
-                              bodies are de-framed in place, http.c:134-160); may be NULL
+                              bodies are de-framed in place, http.c:134-160; a request's
+                              writes stay inside its own [offsets[i], offsets[i+1]), the
+                              bytes around its body rewritten with their own values, so
+                              the caller may fill other requests meanwhile); may be NULL
                               in RHP_MODE_PHR */
   const uint64_t *offsets; /* device: n + 1 offsets, non-decreasing */
   uint64_t        bytes_size; /* readable bytes at `bytes` (>= offsets[n] + RHP_PAD) */

@@ -1867,6 +1867,18 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   __syncthreads();
   dg.replay_start(WAVES);
   if (*wg_deferred) {
+    /* the kernel's arguments loaded again (through an opaque pointer, so the
+     * loads are not merged with the kernel's own): the replay's many uses of
+     * them then keep no scalar registers busy through the loop, where they
+     * were spilled to vector lanes (http kernel: 117 more instructions per
+     * loop iteration, config 5 +4 %) */
+#if defined(__HIP_DEVICE_COMPILE__)   /* the device pass (the host pass only checks the body) */
+    typedef __attribute__((address_space(4))) const Params kParams;
+    kParams *pa = (kParams *) __builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(pa));
+    const Params &p_kernel = p;
+    const Params p = HTTP ? *pa : p_kernel;   /* the phr kernels had no such spills (config 3 +1-3 % with the reload) */
+#endif
     typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
     /* what a request needs first: in http mode the hint left in its http
      * record says what to do (and holds ret), so neither the request record is

@@ -85,3 +85,56 @@ def long_batch():
 
 
 BUILDERS = {"long_batch": long_batch, "edge": lambda: EDGE * 3, "dense": lambda: dense_header_batch(2000, 21)}
+
+
+def chunked_paths_batch(n=6000, seed=11):
+    """Chunked POSTs that take every path of the GPU replay's de-framing
+    (rhp_kernel.hip ChunkWalk / staged_moves / DevMove): 1-8 chunks in a slot
+    (staged), chunks of 1-15 bytes (a block drawing on three or more chunks),
+    9-24 chunks (moved by the lane, second walk), 1-8 chunks beyond a 2 KiB slot
+    (moved by the lane from the kept spans), size lines longer than the 17-20
+    byte window (extensions, OWS, leading zeros), bodies that end at the request's
+    end (the last line reaches into the next request: byte stores), malformed and
+    partial framing, and plain requests between them."""
+    import random
+    rng = random.Random(seed)
+    out = []
+
+    def size_line(sz):
+        h = f"{sz:x}" if rng.random() < 0.7 else f"{sz:X}"
+        r = rng.random()
+        if r < 0.08:
+            h = "0" * rng.randrange(1, 20) + h   # long line: leading zeros
+        elif r < 0.14:
+            h = " " * rng.randrange(1, 4) + h + "\t" * rng.randrange(0, 3)
+        elif r < 0.22:
+            h = h + ";name=" + "v" * rng.randrange(0, 40)   # extension, sometimes past the window
+        return h.encode() + b"\r\n"
+
+    for i in range(n):
+        kind = rng.randrange(10)
+        if kind == 0:
+            out.append(b"GET /g HTTP/1.1\r\nHost: a\r\n\r\n")
+            continue
+        if kind == 1:
+            sizes = [rng.randrange(1, 16) for _ in range(rng.randrange(3, 9))]          # tiny chunks
+        elif kind == 2:
+            sizes = [rng.randrange(1, 200) for _ in range(rng.randrange(9, 25))]        # many chunks
+        elif kind == 3:
+            sizes = [rng.randrange(300, 900) for _ in range(rng.randrange(3, 8))]       # beyond a slot
+        else:
+            sizes = [rng.randrange(1, 400) for _ in range(rng.randrange(1, 9))]         # staged
+        body = b"".join(size_line(s) + bytes(rng.randrange(33, 127) for _ in range(s)) + b"\r\n" for s in sizes)
+        tail = b"0\r\n\r\n"
+        r = rng.random()
+        if r < 0.04:
+            body = body.replace(b"\r\n", b"\n", 1)            # bare LF after a size line
+        elif r < 0.08:
+            body = b"zz\r\n" + body                            # not hex
+        elif r < 0.12:
+            tail = b""                                         # partial: no last chunk
+        elif r < 0.14:
+            tail = b"0;last\n\r\n"
+        head = b"POST /u HTTP/1.1\r\nHost: h\r\nTransfer-Encoding: " + rng.choice([b"chunked", b"Chunked", b"CHUNKED"]) + b"\r\n\r\n"
+        out.append(head + body + tail)
+    return out

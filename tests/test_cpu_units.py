@@ -228,3 +228,15 @@ def test_chunk_window_equals_one_chunk_t():
             if want > 0:
                 assert (doff.value, dlen.value) == (d2.value, l2.value), (line, size)
     assert decided > 50000
+
+
+def test_emulator_chunked_paths_vs_oracle():
+    """The GPU's chunked-paths batch (tests/batches.py chunked_paths_batch) through
+    the kernel emulation: records and rewritten bytes equal the oracle's."""
+    from batches import chunked_paths_batch, pack
+    from oracle_util import assert_same, canon, run_oracle, to_rhp
+    buf, off = pack(chunked_paths_batch(n=3000), align_shift=5)
+    res, _ = rhp.emulate(buf, off, 16, rhp.MODE_HTTP)
+    reqs, hdrs, http, rw = run_oracle(buf, off, 16, rhp.MODE_HTTP)
+    assert_same(canon(res, rhp.MODE_HTTP), to_rhp(reqs, hdrs, http, rhp.MODE_HTTP), buf, off, "emulated chunked paths")
+    assert np.array_equal(res.bytes_out, rw)

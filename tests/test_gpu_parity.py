@@ -11,7 +11,7 @@ import pytest
 import libreactorng_amd as rhp
 from golden_sets import inputs, record_digest
 from oracle_util import assert_same, canon, run_oracle, to_rhp
-from batches import EDGE, dense_header_batch, long_batch, pack
+from batches import EDGE, chunked_paths_batch, dense_header_batch, long_batch, pack
 
 pytestmark = pytest.mark.gpu
 
@@ -139,6 +139,20 @@ def test_gpu_long_inputs_vs_oracle(impl, shift):
                         f"GPU long inputs impl{impl} shift{shift} maxh{maxh} mode{mode}")
             if mode == rhp.MODE_HTTP:
                 assert np.array_equal(res.bytes_out, rw)
+
+
+@pytest.mark.parametrize("shift", [0, 5, 12])
+def test_gpu_chunked_paths_vs_oracle(shift):
+    """Every de-framing path of the replay (staged groups, tiny chunks, many
+    chunks, bodies beyond a slot, long size lines, bodies ending at the request's
+    end, malformed and partial framing), records and rewritten bytes bit-exact
+    vs the oracle (http.c:73-160); a neighbour's bytes are never written."""
+    buf, off = pack(chunked_paths_batch(), align_shift=shift)
+    res = rhp.parse_batch(buf, off, 16, rhp.MODE_HTTP)
+    reqs, hdrs, http, rw = run_oracle(buf, off, 16, rhp.MODE_HTTP)
+    assert_same(canon(res, rhp.MODE_HTTP), to_rhp(reqs, hdrs, http, rhp.MODE_HTTP), buf, off, f"chunked paths shift{shift}")
+    assert np.array_equal(res.bytes_out, rw), f"{int((res.bytes_out != rw).sum())} rewritten bytes differ"
+    assert (http["body_kind"] == 1).sum() > 3000
 
 
 def test_gpu_repeated_launches_rearm_work_counter():

@@ -601,7 +601,7 @@ def main(argv=None):
             # (never `value`, which is device-resident)
             sys.path.insert(0, os.path.join(ROOT, "tools"))
             from e2e_pcie import e2e
-            line["e2e"] = e2e(args.config, per_gpu, reps=5)
+            line["e2e"] = e2e(args.config, per_gpu, reps=7)
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline([args.config] + [k for k in EXTRA_KEYS if k in extra])
         print(json.dumps(line), flush=True)

@@ -65,9 +65,25 @@ def chunk_bounds(n, chunks, taper):
     return out + [n]
 
 
-def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0):
+class MappedHost:
+    """Pinned host memory the kernel writes directly (hipHostMalloc, mapped): the
+    records cross PCIe as the kernel stores them, no D2H copy, no copy engine."""
+
+    def __init__(self, nbytes):
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        self.h, self.d = ctypes.c_void_p(), ctypes.c_void_p()
+        assert self.hip.hipHostMalloc(ctypes.byref(self.h), ctypes.c_size_t(max(nbytes, 1)), ctypes.c_uint(0x2)) == 0
+        assert self.hip.hipHostGetDevicePointer(ctypes.byref(self.d), self.h, ctypes.c_uint(0)) == 0
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(nbytes, 1)).from_address(self.h.value))
+
+    def free(self):
+        self.hip.hipHostFree(self.h)
+
+
+def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0, records="host"):
     """The end-to-end measurement as a dict (bench.py's `e2e` object)."""
-    args = argparse.Namespace(config=config, n=n, chunks=chunks, streams=streams, reps=reps, taper=taper)
+    args = argparse.Namespace(config=config, n=n, chunks=chunks, streams=streams, reps=reps, taper=taper,
+                              records=records)
     cfg = CONFIGS[args.config]
     n, maxh, mode = args.n, cfg["maxh"], cfg["mode"]
     buf, off = rhp.generate(cfg["gen"], n, cfg["seed"])
@@ -88,8 +104,13 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0):
     # contiguous run of (hi - lo) records at hdr_base(k) + r * (hi - lo) * 8
     h_bytes = torch.from_numpy(buf).pin_memory()
     h_off = torch.from_numpy(off.view(np.int64)).pin_memory()
-    h_reqs = torch.empty(n * RS, dtype=torch.uint8).pin_memory()
-    h_hdrs = torch.zeros(hbase[-1], dtype=torch.uint8).pin_memory()
+    zero_copy = args.records == "host"   # the kernel writes the records into mapped host memory
+    if zero_copy:
+        m_reqs, m_hdrs = MappedHost(n * RS), MappedHost(hbase[-1])
+        h_reqs, h_hdrs = torch.from_numpy(m_reqs.array), torch.from_numpy(m_hdrs.array)
+    else:
+        h_reqs = torch.empty(n * RS, dtype=torch.uint8).pin_memory()
+        h_hdrs = torch.zeros(hbase[-1], dtype=torch.uint8).pin_memory()
     d_bytes = torch.empty_like(h_bytes, device=dev)
     d_off = torch.empty_like(h_off, device=dev)
     d_reqs = torch.empty_like(h_reqs, device=dev)
@@ -121,15 +142,16 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0):
                     d_off[lo:hi + 1].copy_(h_off[lo:hi + 1], non_blocking=True)
                 e[1].record(s)
                 if do_kernel:
+                    reqs_p = (m_reqs.d.value if zero_copy else d_reqs.data_ptr()) + RS * lo
+                    hdrs_p = (m_hdrs.d.value if zero_copy else d_hdrs.data_ptr()) + hbase[k]
                     b = rhp.Batch(d_bytes.data_ptr(), d_bytes.data_ptr(), d_off.data_ptr() + 8 * lo, d_bytes.numel(),
-                                  hi - lo, maxh, mode, layout, d_reqs.data_ptr() + RS * lo,
-                                  d_hdrs.data_ptr() + hbase[k],
+                                  hi - lo, maxh, mode, layout, reqs_p, hdrs_p,
                                   d_http.data_ptr() + (rhp.HTTP_DTYPE.itemsize * lo if mode == rhp.MODE_HTTP else 0),
                                   works[k % len(streams)].data_ptr())
                     rc = lib.rhp_parse_batch(ctypes.byref(b), ctypes.c_void_p(s.cuda_stream))
                     assert rc == 0, rc
                 e[2].record(s)
-                if do_d2h:
+                if do_d2h and not zero_copy:
                     h_reqs[RS * lo:RS * hi].copy_(d_reqs[RS * lo:RS * hi], non_blocking=True)
                 e[3].record(s)
             marks.append(e)
@@ -155,7 +177,7 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0):
 
         for k in range(args.chunks):
             lo, hi = bounds[k], bounds[k + 1]
-            if not do_d2h:
+            if not do_d2h or zero_copy:   # zero copy: the kernel wrote the records into host memory
                 continue
             marks[k][3].synchronize()   # chunk k's request records are on the host
             r = reqs_view[lo:hi]
@@ -204,6 +226,8 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0):
 
     t_e2e, tl, d2h_bytes = timed()
     reqs = reqs_view
+    if zero_copy:   # the bytes the kernels wrote over PCIe: request records and used header records
+        d2h_bytes = RS * n + HB * int(reqs["num_headers"][reqs["ret"] > 0].sum())
     ok_frac = float((reqs["ret"] > 0).mean())
     # what came back to the host, against the reference's digest of the same workload
     from bench import golden_spec
@@ -229,10 +253,12 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0):
     h2d_edges = {"before_first_h2d_ms": round(h2d[0][0], 3) if h2d else 0.0,
                  "h2d_idle_gaps_ms": round(sum(max(0.0, b[0] - a[1]) for a, b in zip(h2d, h2d[1:])), 3),
                  "after_last_h2d_ms": round(span - h2d[-1][1], 3) if h2d else 0.0}
-    return ({
+    result = ({
         "config": args.config, "requests": n, "algorithmic_bytes": int(alg), "chunks": args.chunks,
         "streams": args.streams, "ok_fraction": ok_frac,
         "record_layout": ("compact" if layout == rhp.LAYOUT_COMPACT else "header-major") + " per chunk",
+        "records": ("written by the kernels into mapped pinned host memory (no D2H copy)" if args.records == "host"
+                    else "copied back by D2H copies"),
         "parity": parity,
         "taper": args.taper, "chunk_requests": [bounds[k + 1] - bounds[k] for k in range(args.chunks)],
         "e2e_GiBps": round(alg / t_e2e / gib, 2), "e2e_ms": round(t_e2e * 1e3, 3),
@@ -247,6 +273,11 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0):
                          "request records have landed; chunk k+1's speculatively, as many as chunks 0..k used, "
                          "behind its request records when chunk k's are read; more rows on a miss)",
     })
+    if zero_copy:
+        del h_reqs, h_hdrs, reqs_view, reqs
+        m_reqs.free()
+        m_hdrs.free()
+    return result
 
 
 def main():
@@ -257,8 +288,9 @@ def main():
     ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--taper", type=int, default=0)
+    ap.add_argument("--records", default="host", choices=["host", "copy"])
     a = ap.parse_args()
-    print(json.dumps(e2e(a.config, a.n, a.chunks, a.streams, a.reps, a.taper)))
+    print(json.dumps(e2e(a.config, a.n, a.chunks, a.streams, a.reps, a.taper, a.records)))
 
 
 if __name__ == "__main__":

@@ -597,11 +597,19 @@ def main(argv=None):
             line["extra_configs"] = extra
         if world == 1 and args.device == "gpu" and not args.no_e2e:
             # north_star: the path starts and ends in host memory; the rate with
-            # pinned H2D -> kernel -> D2H of the records, chunked over 3 streams
-            # (never `value`, which is device-resident)
-            sys.path.insert(0, os.path.join(ROOT, "tools"))
-            from e2e_pcie import e2e
-            line["e2e"] = e2e(args.config, per_gpu, reps=7)
+            # pinned H2D -> kernel -> records written into mapped host memory,
+            # chunked over 3 streams (never `value`, which is device-resident).
+            # It runs in a child process of its own, as a receiver would: inside
+            # this process (its device copies, streams and allocations) the same
+            # pipeline measured 43 GiB/s with H2D alone 5.3 ms, in its own 47.6-48.5
+            # with H2D alone 5.08 ms (profiles/r04/final/e2e_in_process_vs_child.txt)
+            e2e_cmd = [sys.executable, os.path.join(ROOT, "tools", "e2e_pcie.py"), "--config", args.config,
+                       "--n", str(per_gpu), "--reps", "7"]
+            p = subprocess.run(e2e_cmd, capture_output=True, text=True, timeout=600)
+            if p.returncode != 0:
+                raise RuntimeError("e2e leg failed: " + p.stderr[-2000:])
+            line["e2e"] = json.loads(p.stdout.strip().splitlines()[-1])
+            line["e2e"]["process"] = "a child process of bench.py (tools/e2e_pcie.py)"
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline([args.config] + [k for k in EXTRA_KEYS if k in extra])
         print(json.dumps(line), flush=True)

@@ -65,6 +65,27 @@ def chunk_bounds(n, chunks, taper):
     return out + [n]
 
 
+def numa_diag():
+    """Where the host side runs relative to the GPU: the CPU and NUMA node of the
+    calling thread, and the GPU's NUMA node (sysfs, by its PCI bus id)."""
+    try:
+        libc = ctypes.CDLL("libc.so.6")
+        cpu = libc.sched_getcpu()
+        node = next((int(d[4:]) for d in os.listdir("/sys/devices/system/node") if d.startswith("node")
+                     and os.path.exists(f"/sys/devices/system/node/{d}/cpu{cpu}")), None)
+        hip = ctypes.CDLL("libamdhip64.so")
+        dev = ctypes.c_int()
+        hip.hipGetDevice(ctypes.byref(dev))
+        bus = ctypes.create_string_buffer(64)
+        hip.hipDeviceGetPCIBusId(bus, 64, dev)
+        bid = bus.value.decode().lower()
+        gpu_node = int(open(f"/sys/bus/pci/devices/{bid}/numa_node").read())
+        return {"cpu": cpu, "cpu_node": node, "gpu_pci": bid, "gpu_node": gpu_node,
+                "affinity_cpus": len(os.sched_getaffinity(0))}
+    except Exception as exc:   # diagnostics only
+        return {"error": repr(exc)}
+
+
 class MappedHost:
     """Pinned host memory the kernel writes directly (hipHostMalloc, mapped): the
     records cross PCIe as the kernel stores them, no D2H copy, no copy engine."""
@@ -102,8 +123,17 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0, recor
     # pinned host buffers (the recv side) and full-size device mirrors; chunk k's
     # header records are header-major within the chunk: row r of it is one
     # contiguous run of (hi - lo) records at hdr_base(k) + r * (hi - lo) * 8
-    h_bytes = torch.from_numpy(buf).pin_memory()
-    h_off = torch.from_numpy(off.view(np.int64)).pin_memory()
+    # the receive side: pinned host memory from hipHostMalloc (torch's pin_memory
+    # blocks, taken inside bench.py's long-running process, copied 5 % slower
+    # with idle gaps: H2D alone 5.34 vs 5.09 ms); the copies by hipMemcpyAsync
+    numa = numa_diag()
+    m_bytes, m_off = MappedHost(buf.nbytes), MappedHost(off.nbytes)
+    m_bytes.array[:] = buf
+    m_off.array[:] = off.view(np.uint8)
+    h_bytes = torch.from_numpy(m_bytes.array)
+    h_off = torch.from_numpy(m_off.array.view(np.int64))
+    hip = m_bytes.hip
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
     zero_copy = args.records == "host"   # the kernel writes the records into mapped host memory
     if zero_copy:
         m_reqs, m_hdrs = MappedHost(n * RS), MappedHost(hbase[-1])
@@ -138,8 +168,9 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0, recor
             with torch.cuda.stream(s):
                 e[0].record(s)
                 if do_h2d:
-                    d_bytes[b0:b1].copy_(h_bytes[b0:b1], non_blocking=True)
-                    d_off[lo:hi + 1].copy_(h_off[lo:hi + 1], non_blocking=True)
+                    assert hip.hipMemcpyAsync(d_bytes.data_ptr() + b0, m_bytes.h.value + b0, b1 - b0, 1, s.cuda_stream) == 0
+                    assert hip.hipMemcpyAsync(d_off.data_ptr() + 8 * lo, m_off.h.value + 8 * lo, 8 * (hi + 1 - lo), 1,
+                                              s.cuda_stream) == 0
                 e[1].record(s)
                 if do_kernel:
                     reqs_p = (m_reqs.d.value if zero_copy else d_reqs.data_ptr()) + RS * lo
@@ -260,7 +291,7 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0, recor
         "records": ("written by the kernels into mapped pinned host memory (no D2H copy)" if args.records == "host"
                     else "copied back by D2H copies"),
         "parity": parity,
-        "taper": args.taper, "chunk_requests": [bounds[k + 1] - bounds[k] for k in range(args.chunks)],
+        "numa": numa, "taper": args.taper, "chunk_requests": [bounds[k + 1] - bounds[k] for k in range(args.chunks)],
         "e2e_GiBps": round(alg / t_e2e / gib, 2), "e2e_ms": round(t_e2e * 1e3, 3),
         "kernels_only_GiBps": round(alg / t_kern / gib, 2), "kernels_only_ms": round(t_kern * 1e3, 3),
         "h2d_GBps": round(in_bytes / t_h2d / 1e9, 2), "h2d_ms": round(t_h2d * 1e3, 3),
@@ -273,6 +304,9 @@ def e2e(config="get256", n=1 << 20, chunks=16, streams=3, reps=5, taper=0, recor
                          "request records have landed; chunk k+1's speculatively, as many as chunks 0..k used, "
                          "behind its request records when chunk k's are read; more rows on a miss)",
     })
+    del h_bytes, h_off
+    m_bytes.free()
+    m_off.free()
     if zero_copy:
         del h_reqs, h_hdrs, reqs_view, reqs
         m_reqs.free()

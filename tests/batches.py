@@ -98,7 +98,12 @@ def chunked_paths_batch(n=6000, seed=11):
     partial framing, and plain requests between them."""
     import random
     rng = random.Random(seed)
+    data = np.random.default_rng(seed).integers(33, 127, size=1 << 20, dtype=np.uint8).tobytes()
     out = []
+
+    def payload(sz):
+        at = rng.randrange(0, len(data) - sz)
+        return data[at:at + sz]
 
     def size_line(sz):
         h = f"{sz:x}" if rng.random() < 0.7 else f"{sz:X}"
@@ -124,7 +129,7 @@ def chunked_paths_batch(n=6000, seed=11):
             sizes = [rng.randrange(300, 900) for _ in range(rng.randrange(3, 8))]       # beyond a slot
         else:
             sizes = [rng.randrange(1, 400) for _ in range(rng.randrange(1, 9))]         # staged
-        body = b"".join(size_line(s) + bytes(rng.randrange(33, 127) for _ in range(s)) + b"\r\n" for s in sizes)
+        body = b"".join(size_line(s) + payload(s) + b"\r\n" for s in sizes)
         tail = b"0\r\n\r\n"
         r = rng.random()
         if r < 0.04:

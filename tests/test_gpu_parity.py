@@ -141,18 +141,20 @@ def test_gpu_long_inputs_vs_oracle(impl, shift):
                 assert np.array_equal(res.bytes_out, rw)
 
 
-@pytest.mark.parametrize("shift", [0, 5, 12])
-def test_gpu_chunked_paths_vs_oracle(shift):
+@pytest.mark.parametrize("shift,n", [(0, 6000), (5, 6000), (12, 6000), (3, 160000)])
+def test_gpu_chunked_paths_vs_oracle(shift, n):
     """Every de-framing path of the replay (staged groups, tiny chunks, many
     chunks, bodies beyond a slot, long size lines, bodies ending at the request's
     end, malformed and partial framing), records and rewritten bytes bit-exact
-    vs the oracle (http.c:73-160); a neighbour's bytes are never written."""
-    buf, off = pack(chunked_paths_batch(), align_shift=shift)
+    vs the oracle (http.c:73-160); a neighbour's bytes are never written.  At
+    160K requests a workgroup defers more than its list holds: the second pass
+    then takes the range itself (no first pass)."""
+    buf, off = pack(chunked_paths_batch(n), align_shift=shift)
     res = rhp.parse_batch(buf, off, 16, rhp.MODE_HTTP)
     reqs, hdrs, http, rw = run_oracle(buf, off, 16, rhp.MODE_HTTP)
     assert_same(canon(res, rhp.MODE_HTTP), to_rhp(reqs, hdrs, http, rhp.MODE_HTTP), buf, off, f"chunked paths shift{shift}")
     assert np.array_equal(res.bytes_out, rw), f"{int((res.bytes_out != rw).sum())} rewritten bytes differ"
-    assert (http["body_kind"] == 1).sum() > 3000
+    assert (http["body_kind"] == 1).sum() > n // 2
 
 
 def test_gpu_repeated_launches_rearm_work_counter():

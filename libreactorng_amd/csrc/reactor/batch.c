@@ -34,6 +34,7 @@
 #include <string.h>
 #include <time.h>
 #include <unistd.h>
+#include <poll.h>
 #include <sys/eventfd.h>
 #include <hip/hip_runtime_api.h>
 
@@ -98,6 +99,11 @@ typedef struct batch_state
   /* the waiter / worker thread: started once, stopped and joined at teardown */
   int             have_worker, stop;
   hipStream_t     cstream;   /* gpu: D2H of a round's de-framed bytes, when it has chunked bodies */
+  int             delay_us;   /* RHP_REACTOR_DELAY_COMPLETION_US (tests): the completion thread sleeps before its write */
+  /* the host-batch writer's reply buffer and offsets (freed at teardown) */
+  buffer_t        hb_buf;
+  uint64_t       *hb_off;
+  size_t          hb_cap;
 } batch_state_t;
 
 /* One parser per reactor thread, on the heap: the waiter / worker thread holds
@@ -121,6 +127,39 @@ static int      st_on;
 
 static void host_parse(batch_state_t *b, int k);
 
+/* The worker / waiter has finished the round at the head of the queue: the
+ * eventfd is written BEFORE the entry leaves the queue, so once
+ * reactor_batch_wait has seen the queue empty every completion is on the
+ * eventfd (written after it, the last warm-up round's write could
+ * land after reactor_batch_prepare drained the eventfd and finish the first
+ * real round early).  The loop thread may hear of the round and submit its
+ * slot again before the entry leaves: reactor_batch_submit waits for room.
+ * Called with b->mu unlocked; returns with it locked. */
+static void round_complete(batch_state_t *b)
+{
+  if (b->delay_us)   /* test knob: a late completion write (RHP_REACTOR_DELAY_COMPLETION_US) */
+    usleep((useconds_t) b->delay_us);
+  const uint64_t one = 1;
+  ssize_t r = write(b->efd, &one, sizeof one);
+  (void) r;
+  pthread_mutex_lock(&b->mu);
+  b->q_head = (b->q_head + 1) % REACTOR_BATCH_SLOTS;
+  b->q_n--;
+  pthread_cond_broadcast(&b->cv);
+}
+
+/* queue slot k for the worker / waiter (in submission order) */
+static void queue_slot(batch_state_t *b, int k)
+{
+  pthread_mutex_lock(&b->mu);
+  while (b->q_n >= REACTOR_BATCH_SLOTS)   /* a completed round whose entry has not left yet */
+    pthread_cond_wait(&b->cv, &b->mu);
+  b->q[(b->q_head + b->q_n) % REACTOR_BATCH_SLOTS] = k;
+  b->q_n++;
+  pthread_cond_broadcast(&b->cv);
+  pthread_mutex_unlock(&b->mu);
+}
+
 /* host-async worker: the state is its creator's (B is per thread) */
 static void *host_worker(void *arg)
 {
@@ -135,17 +174,7 @@ static void *host_worker(void *arg)
     const int k = b->q[b->q_head];
     pthread_mutex_unlock(&b->mu);
     host_parse(b, k);
-    /* the entry leaves the queue before the loop thread hears of the round:
-     * it may finish the slot and submit it again right after the write */
-    pthread_mutex_lock(&b->mu);
-    b->q_head = (b->q_head + 1) % REACTOR_BATCH_SLOTS;
-    b->q_n--;
-    pthread_cond_broadcast(&b->cv);
-    pthread_mutex_unlock(&b->mu);
-    const uint64_t one = 1;
-    ssize_t r = write(b->efd, &one, sizeof one);
-    (void) r;
-    pthread_mutex_lock(&b->mu);
+    round_complete(b);
   }
   pthread_mutex_unlock(&b->mu);
   return NULL;
@@ -174,15 +203,7 @@ static void *gpu_waiter(void *arg)
     }
     else
       (void) hipEventSynchronize(b->ev[k]);
-    pthread_mutex_lock(&b->mu);
-    b->q_head = (b->q_head + 1) % REACTOR_BATCH_SLOTS;
-    b->q_n--;
-    pthread_cond_broadcast(&b->cv);
-    pthread_mutex_unlock(&b->mu);
-    const uint64_t one = 1;
-    ssize_t r = write(b->efd, &one, sizeof one);
-    (void) r;
-    pthread_mutex_lock(&b->mu);
+    round_complete(b);
   }
   pthread_mutex_unlock(&b->mu);
   return NULL;
@@ -237,6 +258,8 @@ static int parser(void)
     const char *e = getenv("RHP_REACTOR_PARSER");
     B->parser = !e ? PARSER_GPU : strcmp(e, "host") == 0 ? PARSER_HOST : strcmp(e, "host-async") == 0 ? PARSER_HOST_ASYNC
                                                                                                        : PARSER_GPU;
+    const char *dl = getenv("RHP_REACTOR_DELAY_COMPLETION_US");
+    B->delay_us = dl ? atoi(dl) : 0;
     const char *dg = getenv("RHP_REACTOR_DIAG");
     B->diag_host = dg && strcmp(dg, "hostparse") == 0;
     B->efd = -1;
@@ -406,13 +429,7 @@ void reactor_batch_submit(int k, uint32_t n, size_t bytes, uint32_t n_sessions)
   s->h_off[n] = bytes;
   if (B->parser == PARSER_HOST_ASYNC)
   {
-    pthread_mutex_lock(&B->mu);
-    if (B->q_n >= REACTOR_BATCH_SLOTS)
-      die("reactor_batch_submit: queue full", B->q_n);
-    B->q[(B->q_head + B->q_n) % REACTOR_BATCH_SLOTS] = k;
-    B->q_n++;
-    pthread_cond_broadcast(&B->cv);
-    pthread_mutex_unlock(&B->mu);
+    queue_slot(B, k);
     return;
   }
   if (B->parser == PARSER_HOST || B->diag_host)
@@ -449,13 +466,7 @@ void reactor_batch_submit(int k, uint32_t n, size_t bytes, uint32_t n_sessions)
     return;
   }
   HIP(hipEventRecord(B->ev[k], B->stream));
-  pthread_mutex_lock(&B->mu);
-  if (B->q_n >= REACTOR_BATCH_SLOTS)
-    die("reactor_batch_submit: queue full", B->q_n);
-  B->q[(B->q_head + B->q_n) % REACTOR_BATCH_SLOTS] = k;
-  B->q_n++;
-  pthread_cond_broadcast(&B->cv);
-  pthread_mutex_unlock(&B->mu);
+  queue_slot(B, k);
 }
 
 int reactor_batch_completed(void)
@@ -562,16 +573,16 @@ void reactor_batch_write(const uint8_t *arena, size_t arena_n, const rhp_resp_t 
 {
   if (B->writer - 1 == WRITER_HOST_BATCH)
   {
-    /* the host serializer, into one buffer in reply order */
-    static __thread buffer_t buf;
-    static __thread uint64_t *off;
-    static __thread size_t cap;
-    if (n + 1 > cap)
+    /* the host serializer, into one buffer in reply order (the thread's
+     * parser state holds it: batch_teardown frees it) */
+    buffer_t buf = B->hb_buf;
+    if (n + 1 > B->hb_cap)
     {
-      cap = n + 1 > 2 * cap ? n + 1 : 2 * cap;
-      if (!(off = realloc(off, cap * sizeof *off)))
+      B->hb_cap = n + 1 > 2 * B->hb_cap ? n + 1 : 2 * B->hb_cap;
+      if (!(B->hb_off = realloc(B->hb_off, B->hb_cap * sizeof *B->hb_off)))
         abort();
     }
+    uint64_t *off = B->hb_off;
     buffer_clear(&buf);
     stream_t tmp;   /* http_write_response appends to a stream's output buffer */
     memset(&tmp, 0, sizeof tmp);
@@ -589,8 +600,8 @@ void reactor_batch_write(const uint8_t *arena, size_t arena_n, const rhp_resp_t 
                           data(arena + r->type.off, r->type.len), data(arena + r->body.off, r->body.len), f, nf);
     }
     off[n] = buffer_size(&tmp.output);
-    buf = tmp.output;
-    *out = buffer_base(&buf);
+    B->hb_buf = tmp.output;
+    *out = buffer_base(&B->hb_buf);
     *out_off = off;
     (void) arena_n;
     (void) n_fields;
@@ -698,8 +709,20 @@ static void batch_teardown(void *arg)
   }
   if (b->efd >= 0)
     close(b->efd);
+  buffer_destruct(&b->hb_buf);
+  free(b->hb_off);
   free(b);
   B = NULL;
+}
+
+void reactor_batch_release(void)
+{
+  if (!B)
+    return;
+  /* on the owning thread, while the HIP runtime's per-thread state is intact;
+   * the key's destructor is the fallback for threads that exit without it */
+  (void) pthread_setspecific(batch_key, NULL);
+  batch_teardown(B);
 }
 
 void reactor_batch_prepare(void)
@@ -722,8 +745,16 @@ void reactor_batch_prepare(void)
     ss[0].piece_hi = 1;
     reactor_batch_submit(k, 1, n, 1);
   }
+  /* the warm-up rounds' completions are nobody's: exactly that many are read
+   * off the eventfd, waiting for each (whatever the completion path) */
+  for (int left = REACTOR_BATCH_SLOTS; left > 0;)
+  {
+    struct pollfd pfd = {.fd = B->efd, .events = POLLIN};
+    if (poll(&pfd, 1, -1) < 0 && errno != EINTR)
+      die("poll", errno);
+    uint64_t v = 0;
+    if (read(B->efd, &v, sizeof v) == (ssize_t) sizeof v)
+      left -= (int) v;
+  }
   reactor_batch_wait();
-  uint64_t v;
-  while (read(B->efd, &v, sizeof v) == (ssize_t) sizeof v)
-    ;   /* the warm-up rounds' completions are nobody's */
 }

@@ -34,6 +34,10 @@ int       reactor_batch_async(void);
  * client's first burst pays for them */
 void      reactor_batch_prepare(void);
 int       reactor_batch_fd(void);
+/* the thread's parser state (streams, events, pinned and device slots, the
+ * completion thread) released on this thread, e.g. when its last server goes;
+ * every round must be complete.  The next round sets it up again. */
+void      reactor_batch_release(void);
 /* staging of slot k for `bytes` packed input bytes (+ RHP_PAD), n pieces and
  * n_sessions sessions */
 uint8_t  *reactor_batch_reserve(int k, size_t bytes, uint32_t n, uint32_t n_sessions);

@@ -289,26 +289,70 @@ RHP_DHD constexpr uint32_t state2(uint32_t idx)
 {
   return (idx & 2u) ? (idx >> 2) + S_NUM_PLAIN : idx >> 2;
 }
-enum : uint32_t {
-  kRows2 = 4u * (S_NUM_PLAIN - 1u) + 2u,          /* highest index (last plain state, e = 1) + 1 */
-  kClassRow = 4u * (S_COUNT - S_NUM_PLAIN) + 2u,   /* first index no state uses */
-  kTable2Bytes = kRows2 * 256u
-};
-static_assert(kClassRow < kRows2 && state2(kClassRow) >= S_COUNT, "class row is a hole");
 
 /*
- * Pair codes by two lookups instead of arithmetic (the kernel's RHP_CODE2 form):
+ * Row geometry.  The row of pair index idx starts at LDS byte idx * kStride and
+ * holds entries for the codes class(b0) * 16 + class(b1) < kCodes.  With a
+ * stride of 256 the walk's address is one v_perm (idx * 256 + code), and every
+ * row starts in LDS bank 0: lanes in different states reading the same code
+ * read the same bank at different addresses, an N-way conflict in the walk's
+ * dependent read.  A stride of 260 (RHP_ROW_STRIDE) starts row idx one bank
+ * further (one v_mad_u32_u24 instead of the v_perm).
+ */
+#ifndef RHP_ROW_STRIDE
+#define RHP_ROW_STRIDE 256
+#endif
+enum : uint32_t {
+  kStride = RHP_ROW_STRIDE,
+  kCodes = (kClasses - 1u) * 16u + kClasses,      /* highest code + 1 */
+  kRows2 = 4u * (S_NUM_PLAIN - 1u) + 2u           /* highest index (last plain state, e = 1) + 1 */
+};
+static_assert(kStride >= 256u && kStride % 4u == 0, "rows hold every code, dword aligned");
+static_assert(kRows2 <= 256u, "indices are bytes");
+
+/* the indices a state uses: plain states 4s, 4s+1; event states 4(s - S_NUM_PLAIN) + 2, + 3 */
+RHP_DHD constexpr bool idx_used(uint32_t i) { return i < kRows2 && state2(i) < S_COUNT; }
+
+/*
+ * Pair codes by two lookups instead of arithmetic:
  *   r    = T[kClassRowR * 256 + b1]     the row of class(b1): code_row(class(b1))
  *   code = T[r * 256 + b0]              = class(b0) * 16 + class(b1)
- * so a pair costs two address v_perms and no packing ops.  The rows live in
- * holes of the pair table (plain-state rows 4s+2, 4s+3, s >= 8, no state uses).
+ * so a pair costs two address v_perms and no packing ops.  These rows (and the
+ * byte-class row kClassRow) are 256-byte aligned (a v_perm builds their
+ * addresses) and placed in the holes the state rows leave: the first free
+ * 256-byte rows.
  */
-RHP_DHD constexpr uint32_t code_row(uint32_t k) { return 4u * (9u + k) + 2u; }   /* k < kClasses */
-enum : uint32_t { kClassRowR = kClassRow + 1u };
-static_assert(kClassRowR < kRows2 && state2(kClassRowR) >= S_COUNT, "class-row row is a hole");
-static_assert(code_row(kClasses - 1u) < kRows2 && state2(code_row(0)) >= S_COUNT &&
-              state2(code_row(kClasses - 1u)) >= S_COUNT, "code rows are holes");
-static_assert(kRows2 <= 256u, "indices are bytes");
+struct RowLayout {
+  uint32_t row[2 + kClasses];   /* kClassRow, kClassRowR, code_row(0..14) */
+  uint32_t bytes;               /* the table's size, 16-byte multiple */
+};
+constexpr RowLayout make_row_layout()
+{
+  RowLayout l{};
+  uint32_t end = 0, n = 0;
+  for (uint32_t i = 0; i < kRows2; i++)
+    if (idx_used(i) && i * kStride + kCodes > end) end = i * kStride + kCodes;
+  for (uint32_t r = 0; r < 256u && n < 2u + kClasses; r++) {
+    bool free = true;
+    for (uint32_t i = 0; i < kRows2; i++)
+      if (idx_used(i) && i * kStride < r * 256u + 256u && r * 256u < i * kStride + kCodes) free = false;
+    if (free) {
+      l.row[n++] = r;
+      if (r * 256u + 256u > end) end = r * 256u + 256u;
+    }
+  }
+  l.bytes = n == 2u + kClasses ? (end + 15u) & ~15u : 0u;
+  return l;
+}
+constexpr RowLayout kRowLayout = make_row_layout();
+static_assert(kRowLayout.bytes != 0, "the lookup rows fit");
+enum : uint32_t {
+  kClassRow = kRowLayout.row[0],
+  kClassRowR = kRowLayout.row[1],
+  kTable2Bytes = kRowLayout.bytes
+};
+RHP_DHD constexpr uint32_t code_row(uint32_t k) { return kRowLayout.row[2 + k]; }   /* k < kClasses */
+static_assert(kClassRowR < 256u && code_row(kClasses - 1u) < 256u, "row numbers are bytes");
 
 RHP_DHD constexpr bool is_done2(uint32_t i) { return state2(i) == S_DONE || state2(i) == S_DONE_E; }
 RHP_DHD constexpr bool is_err2(uint32_t i) { return state2(i) == S_ERR || state2(i) == S_ERR_E; }
@@ -325,15 +369,11 @@ constexpr Table2 make_table2()
   for (uint32_t s = 0; s < S_COUNT; s++) {
     const bool ev = s >= S_NUM_PLAIN;
     for (uint32_t e = ev ? 2u : 0u; e < (ev ? 4u : 2u); e++) {
-      const uint32_t row = idx2(s, e) * 256u;
-      for (uint32_t k0 = 0; k0 < 16; k0++)
-        for (uint32_t k1 = 0; k1 < 16; k1++) {
-          uint32_t next = idx2(S_SLOW, 0);
-          if (k0 < kClasses && k1 < kClasses) {
-            const uint32_t s1 = step(s, class_rep(k0)), s2 = step(s1, class_rep(k1));
-            next = idx2(s2, (s1 >= S_NUM_PLAIN ? 1u : 0u) | (s2 >= S_NUM_PLAIN ? 2u : 0u));
-          }
-          t.b[row + k0 * 16u + k1] = (uint8_t) next;
+      const uint32_t row = idx2(s, e) * kStride;
+      for (uint32_t k0 = 0; k0 < kClasses; k0++)
+        for (uint32_t k1 = 0; k1 < kClasses; k1++) {
+          const uint32_t s1 = step(s, class_rep(k0)), s2 = step(s1, class_rep(k1));
+          t.b[row + k0 * 16u + k1] = (uint8_t) idx2(s2, (s1 >= S_NUM_PLAIN ? 1u : 0u) | (s2 >= S_NUM_PLAIN ? 2u : 0u));
         }
     }
   }

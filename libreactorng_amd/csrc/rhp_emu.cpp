@@ -106,7 +106,7 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
       for (int w = 0; w < words; w++) {
         uint32_t ev = 0;
         for (int k = 0; k < 32; k += 2) {   /* one table read per byte pair */
-          st = T.b[st * 256u + cls[win[32 * w + k]] * 16u + cls[win[32 * w + k + 1]]];
+          st = T.b[st * kStride + cls[win[32 * w + k]] * 16u + cls[win[32 * w + k + 1]]];
           ev |= (st & 3u) << k;
         }
         evw[w] = ev;

@@ -881,6 +881,14 @@ __device__ __forceinline__ uint32_t lds_u8(uint32_t a)
   return *reinterpret_cast<const __attribute__((address_space(3))) uint8_t *>((size_t) a);
 }
 
+/* LDS address of pair index st's entry for code c (rhp_dfa.h row geometry):
+ * st * 256 + c is one v_perm; another stride one v_mad_u32_u24 */
+__device__ __forceinline__ uint32_t row_addr(uint32_t st, uint32_t c)
+{
+  if constexpr (kStride == 256u) return __builtin_amdgcn_perm(st, c, 0x0c0c0400u);
+  else return __umul24(st, kStride) + c;
+}
+
 /* keep the compiler from sinking the computation of x into a branch */
 __device__ __forceinline__ void opaque(uint32_t &x) { asm("" : "+v"(x)); }
 
@@ -1563,7 +1571,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       uint32_t cn[8];
 #pragma unroll
       for (int j = 0; j < 8; j++) {
-        st = lds_u8(__builtin_amdgcn_perm(st, c[j], 0x0c0c0400u));
+        st = lds_u8(row_addr(st, c[j]));
         __builtin_amdgcn_sched_barrier(0);   /* the chained read issues first */
         if (nx)
           r[j] = lds_u8(__builtin_amdgcn_perm(kClassRowR, W[q + 1][j >> 1], 0x0c0c0400u | (uint32_t) (2 * (j & 1) + 1)));

@@ -132,6 +132,19 @@ def test_server_cases_gpu_batch_parser(writer, monkeypatch):
     assert "config1 16 pipelined   responses 16  callbacks 16" in out
 
 
+@pytest.mark.parametrize("parser", ["host-async", pytest.param("gpu", marks=pytest.mark.gpu)])
+def test_server_first_round_after_late_completion(parser, monkeypatch):
+    """the completion thread writes the eventfd before its queue
+    entry leaves, so a round's completion is never still in flight when the
+    queue looks empty (server_open's warm-up drains exactly its own rounds;
+    a teardown drains all).  With every completion write held back 3 ms the
+    first real rounds after server_open (the reference's cases first) and the
+    load must still get their own replies."""
+    monkeypatch.setenv("RHP_REACTOR_DELAY_COMPLETION_US", "3000")
+    out = _run([os.path.join(BIN, "server_test"), "8", "16"], parser)
+    assert f"parser: {parser}" in out and "OK (0 failures)" in out
+
+
 def test_server_thread_exit_host_async():
     """A reactor thread serving with the asynchronous parser exits, three times
     over: its parser state (the worker thread, slots, eventfd) is torn down by

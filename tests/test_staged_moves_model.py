@@ -105,3 +105,96 @@ def test_staged_moves_model_matches_oracle():
             work[a] = v
     assert staged > n * 0.8
     assert np.array_equal(work, want), f"{int((work != want).sum())} bytes differ from the oracle's"
+
+
+K_STAGE_BODIES = 4
+
+
+def group_schedule(m):
+    """rhp_kernel.hip staged_moves' hand-out, step by step: take() fills the
+    four slots of a group from the lowest set bits of the mask m (a slot with
+    no body left gets have bit 0 and the group's first owner, which is a valid
+    lane whenever any slot holds a body; an all-empty group's owners stay
+    unset: None here), the loop loads a group only when it holds a body and
+    ends at the first empty one.  Returns the groups as (owners, have) in
+    processing order, asserting what the kernel relies on."""
+    groups = []
+
+    def take(prev_owner0):
+        nonlocal m
+        owner, have = [None] * K_STAGE_BODIES, 0
+        for q in range(K_STAGE_BODIES):
+            owner[q] = (m & -m).bit_length() - 1 if m else (owner[0] if q else prev_owner0)
+            if m:
+                have |= 1 << q
+            m &= (m - 1) if m else 0
+        return owner, have
+
+    g = take(None)   # the call site runs staged_moves only for m != 0
+    assert g[1], "the first group holds a body"
+    while g[1]:
+        groups.append(g)
+        gn = take(None)   # the kernel's Group gn is fresh: an empty group's owner[0] is unset (never read)
+        g = gn
+    return groups
+
+
+def test_staged_moves_group_take_model():
+    rng = np.random.default_rng(7)
+    masks = [1, 1 << 63, (1 << 64) - 1, 0b1011, 0b1111, 0b11111, (1 << 63) | 1, 0x8000_0000_0000_0007]
+    masks += [int(rng.integers(1, 1 << 63)) | (int(rng.integers(0, 2)) << 63) for _ in range(2000)]
+    masks += [(1 << k) - 1 for k in range(1, 65)] + [((1 << k) - 1) << (64 - k) for k in range(1, 65)]
+    for m0 in masks:
+        lanes = [j for j in range(64) if m0 >> j & 1]
+        groups = group_schedule(m0)
+        taken = []
+        for owner, have in groups:
+            assert have & (have + 1) == 0, "the slots holding bodies are the low ones"
+            nb = bin(have).count("1")
+            taken += owner[:nb]
+            # every slot's loads address a staged lane's body (an empty slot: the group's first body, one line)
+            assert all(o in lanes for o in owner), (hex(m0), owner, have)
+            assert owner[nb:] == [owner[0]] * (K_STAGE_BODIES - nb)
+        assert taken == lanes, "every staged body is built once, in lane order"
+        assert len(groups) == -(-len(lanes) // K_STAGE_BODIES)
+
+
+def test_staged_moves_partial_groups_rebuild_bodies():
+    """Bodies of the chunked workload staged by lanes with gaps in the mask,
+    group by group as the schedule hands them out (partial last groups, empty
+    slots loading another body's first line): the stores rebuild the oracle's
+    bytes."""
+    n = 512
+    buf, off = rhp.generate(rhp.GEN_CHUNKED, n, 99)
+    reqs, _, http, want = run_oracle(buf, off, 16, rhp.MODE_HTTP)
+    work = buf.copy()
+    bodies = []
+    for i in range(n):
+        if http["result"][i] != 1 or not http["body_kind"][i]:
+            continue
+        base, end = int(off[i]) + int(reqs["ret"][i]), int(off[i + 1])
+        spans, region = chunk_spans(buf, base, end)
+        L = sum(x for _, x in spans)
+        if len(spans) > K_MOVE_CHUNKS or (base & 15) + region + 20 > K_STAGE_BODY:
+            work[base:base + L] = want[base:base + L]
+            continue
+        bodies.append((base, spans, region, end - base, int(off[i])))
+    rng = np.random.default_rng(3)
+    k = 0
+    while k < len(bodies):
+        # a round of 64 lanes: some lanes staged a body, the others did not
+        m = int(rng.integers(1, 1 << 63))
+        lanes = [j for j in range(64) if m >> j & 1]
+        lane_body = {j: bodies[k + t] for t, j in enumerate(lanes[:len(bodies) - k])}
+        m = sum(1 << j for j in lane_body)
+        for owner, have in group_schedule(m):
+            nb = bin(have).count("1")
+            for q in range(K_STAGE_BODIES):   # every slot loads: an empty one the first body's first line
+                base = lane_body[owner[q]][0]
+                la = base & ~15
+                assert 0 <= la and la + 16 <= len(buf)
+            stores = [s for q in range(nb) for s in staged_body(buf, *lane_body[owner[q]])]
+            for a, v in stores:   # a group's loads land before its stores
+                work[a] = v
+        k += len(lane_body)
+    assert np.array_equal(work, want), f"{int((work != want).sum())} bytes differ from the oracle's"

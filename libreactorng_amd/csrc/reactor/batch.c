@@ -66,6 +66,11 @@ typedef struct slot
   uint32_t     n, n_sess;
   size_t       bytes;
   uint64_t     t_submit;
+  /* RHP_REACTOR_STATS=2 (the per-phase timeline): timing events around the
+   * round's H2D, parse, fix-up and D2H, and host clocks of its submit's end and
+   * of the completion thread's wake-up */
+  hipEvent_t   tev[5];
+  uint64_t     t_enqueued, t_wake;
 } slot_t;
 
 typedef struct batch_state
@@ -124,8 +129,15 @@ static void batch_key_init(void)
  * thread, printed at exit */
 static uint64_t st_rounds, st_requests, st_ns;
 static int      st_on;
+/* RHP_REACTOR_STATS=2: sums over the rounds, ns (device phases from the events) */
+enum { PH_SUBMIT, PH_H2D, PH_PARSE, PH_FIXUP, PH_D2H, PH_DEVICE, PH_WAKE, PH_LOOP, PH_COUNT };
+static uint64_t st_phase[PH_COUNT], st_tl_rounds;
+static const char *const st_phase_name[PH_COUNT] = {
+  "submit (host: H2D, kernels, D2H enqueued)", "H2D", "rhp_parse_batch", "rhp_fixup_sessions", "D2H records",
+  "device span (H2D start -> D2H end)", "submit -> completion thread awake", "completion thread -> loop takes the result"};
 
 static void host_parse(batch_state_t *b, int k);
+static uint64_t now_ns(void);
 
 /* The worker / waiter has finished the round at the head of the queue: the
  * eventfd is written BEFORE the entry leaves the queue, so once
@@ -203,6 +215,8 @@ static void *gpu_waiter(void *arg)
     }
     else
       (void) hipEventSynchronize(b->ev[k]);
+    if (st_on == 2)
+      b->slot[k].t_wake = now_ns();
     round_complete(b);
   }
   pthread_mutex_unlock(&b->mu);
@@ -218,6 +232,13 @@ static uint64_t now_ns(void)
 
 static void print_stats(void)
 {
+  const uint64_t tr = __atomic_load_n(&st_tl_rounds, __ATOMIC_RELAXED);
+  if (st_on == 2 && tr)
+  {
+    fprintf(stderr, "reactor round timeline (mean over %llu gpu rounds, us):\n", (unsigned long long) tr);
+    for (int k = 0; k < PH_COUNT; k++)
+      fprintf(stderr, "  %-48s %9.1f\n", st_phase_name[k], (double) st_phase[k] / 1e3 / (double) tr);
+  }
   const uint64_t r = __atomic_load_n(&st_rounds, __ATOMIC_RELAXED), q = __atomic_load_n(&st_requests, __ATOMIC_RELAXED);
   const uint64_t ns = __atomic_load_n(&st_ns, __ATOMIC_RELAXED);
   fprintf(stderr, "reactor parser %s: %llu rounds, %llu requests (%.1f per round), %.1f us per round (submit to result)\n",
@@ -237,7 +258,7 @@ static void die(const char *what, int e)
 static void stats_init(void)
 {
   const char *st = getenv("RHP_REACTOR_STATS");
-  if ((st_on = st && *st == '1'))
+  if ((st_on = st && (*st == '1' || *st == '2') ? *st - '0' : 0))
     atexit(print_stats);
 }
 
@@ -439,7 +460,17 @@ void reactor_batch_submit(int k, uint32_t n, size_t bytes, uint32_t n_sessions)
       round_done((void *) (intptr_t) B->efd);   /* diagnostic mode keeps the asynchronous protocol */
     return;
   }
+  const bool tl = st_on == 2;
+  if (tl)
+  {
+    if (!s->tev[0])
+      for (int e = 0; e < 5; e++)
+        HIP(hipEventCreate(&s->tev[e]));
+    HIP(hipEventRecord(s->tev[0], B->stream));
+  }
   HIP(hipMemcpyAsync(s->d_buf, s->h_buf, s->in_size, hipMemcpyHostToDevice, B->stream));   /* bytes, offsets, sessions */
+  if (tl)
+    HIP(hipEventRecord(s->tev[1], B->stream));
   /* the pieces speculatively, then every session walked in order from its
    * true request boundaries (include/rhp.h rhp_fixup_sessions): all of a
    * round's pipelined requests, bodies included, in this one round */
@@ -452,14 +483,23 @@ void reactor_batch_submit(int k, uint32_t n, size_t bytes, uint32_t n_sessions)
   int rc = rhp_parse_batch(&b, B->stream);
   if (rc != 0)
     die("rhp_parse_batch", rc);
+  if (tl)
+    HIP(hipEventRecord(s->tev[2], B->stream));
   rc = rhp_fixup_sessions(&b, (const rhp_session_t *) (d + s->o_sess), n_sessions,
                           (rhp_session_result_t *) (d + s->o_sres), (uint64_t *) (d + s->o_start), B->stream);
   if (rc != 0)
     die("rhp_fixup_sessions", rc);
+  if (tl)
+    HIP(hipEventRecord(s->tev[3], B->stream));
   /* the records: one asynchronous copy of the layout's output part (the
    * bytes, de-framed in place where a body is chunked, http.c:155, come back
    * only for a round that has such a body: reactor_batch_result) */
   HIP(hipMemcpyAsync(s->h_buf + s->o_req, s->d_buf + s->o_req, s->out_size - s->o_req, hipMemcpyDeviceToHost, B->stream));
+  if (tl)
+  {
+    HIP(hipEventRecord(s->tev[4], B->stream));
+    s->t_enqueued = now_ns();
+  }
   if (B->complete == COMPLETE_HOSTFUNC)
   {
     HIP(hipLaunchHostFunc(B->stream, round_done, (void *) (intptr_t) B->efd));
@@ -499,7 +539,23 @@ void reactor_batch_result(int k, reactor_batch_result_t *out)
   {
     __atomic_fetch_add(&st_rounds, 1, __ATOMIC_RELAXED);
     __atomic_fetch_add(&st_requests, s->n, __ATOMIC_RELAXED);
-    __atomic_fetch_add(&st_ns, now_ns() - s->t_submit, __ATOMIC_RELAXED);
+    const uint64_t t_result = now_ns();
+    __atomic_fetch_add(&st_ns, t_result - s->t_submit, __ATOMIC_RELAXED);
+    if (st_on == 2 && B->parser == PARSER_GPU && s->tev[0] && s->t_wake)
+    {
+      float ms[5] = {0, 0, 0, 0, 0};
+      for (int e = 1; e < 5; e++)
+        (void) hipEventElapsedTime(&ms[e], s->tev[e - 1], s->tev[e]);
+      float span = 0;
+      (void) hipEventElapsedTime(&span, s->tev[0], s->tev[4]);
+      const uint64_t add[PH_COUNT] = {s->t_enqueued - s->t_submit, (uint64_t) (ms[1] * 1e6f), (uint64_t) (ms[2] * 1e6f),
+                                      (uint64_t) (ms[3] * 1e6f), (uint64_t) (ms[4] * 1e6f), (uint64_t) (span * 1e6f),
+                                      s->t_wake - s->t_submit, t_result - s->t_wake};
+      for (int k2 = 0; k2 < PH_COUNT; k2++)
+        __atomic_fetch_add(&st_phase[k2], add[k2], __ATOMIC_RELAXED);
+      __atomic_fetch_add(&st_tl_rounds, 1, __ATOMIC_RELAXED);
+      s->t_wake = 0;
+    }
   }
   if (B->parser == PARSER_GPU && !B->diag_host)
   {
@@ -678,6 +734,9 @@ static void batch_teardown(void *arg)
   }
   for (int k = 0; k < REACTOR_BATCH_SLOTS; k++)
   {
+    if (b->parser == PARSER_GPU && b->slot[k].tev[0])
+      for (int e = 0; e < 5; e++)
+        (void) hipEventDestroy(b->slot[k].tev[e]);
     host_free(b->slot[k].h_buf);
     if (b->parser == PARSER_GPU)
       dev_free((void **) &b->slot[k].d_buf);

@@ -317,7 +317,7 @@ void reactor_loop_once(void)
   if (core_stats < 0)
   {
     const char *st = getenv("RHP_REACTOR_STATS");
-    core_stats = st && *st == '1';
+    core_stats = st && (*st == '1' || *st == '2');
     if (core_stats)
       atexit(core_print_stats);
   }

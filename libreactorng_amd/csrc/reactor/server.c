@@ -412,7 +412,7 @@ static void round_stats_init(void)
   if (round_stats < 0)
   {
     const char *st = getenv("RHP_REACTOR_STATS");
-    if ((round_stats = st && *st == '1'))
+    if ((round_stats = st && (*st == '1' || *st == '2')))
       atexit(rs_print);
   }
 }

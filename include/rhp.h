@@ -81,9 +81,10 @@ typedef struct rhp_hdr {
 enum rhp_layout {
   RHP_LAYOUT_REQUEST_MAJOR = 0,
   RHP_LAYOUT_HEADER_MAJOR = 1,
-  RHP_LAYOUT_COMPACT = 2      /* RHP_MODE_PHR: 4-byte records, below */
+  RHP_LAYOUT_COMPACT = 2      /* 4-byte header records, below (http mode: 8-byte http records too;
+                                 not with RHP_BATCH_SPECULATIVE) */
 };
-/* Compact records (RHP_LAYOUT_COMPACT, RHP_MODE_PHR).  A header line the DFA
+/* Compact records (RHP_LAYOUT_COMPACT).  A header line the DFA
  * parses is `name ": " value CRLF` and the first one starts right after the
  * request line `method SP path SP "HTTP/1." digit CRLF`, so its record is two
  * lengths: hdrs holds u32 lens[max_headers][n] (header-major), name_len |
@@ -114,6 +115,27 @@ typedef struct rhp_http {
   uint64_t body_len;
 } rhp_http_t;
 
+/* Compact http records (RHP_LAYOUT_COMPACT, RHP_MODE_HTTP): http holds
+ * rhp_http_compact_t hc[n] (8 B) and, at byte RHP_COMPACT_HTTP_WIDE_OFF(n), a
+ * wide area rhp_http_t wide[n]; RHP_COMPACT_HTTP_BYTES(n) bytes in all.  A
+ * record without RHP_HTTP_WIDE holds result, body_kind and body_len, and
+ * consumed = ret + (body_kind == 1 ? body_len : 0) for result 1, else 0 (the
+ * DFA path's framing: no body, or a Content-Length body).  A record with
+ * RHP_HTTP_WIDE (the exact path, a chunked body de-framed in place) is
+ * wide[i].  rhp_expand_http (rhp_host.h) turns them into rhp_http_t.  With
+ * the compact header records, a uniform batch writes 16 + 4 h + 8 bytes per
+ * request (config 5: 40 B, was 16 + 8 h + 24 = 70 B header-major). */
+typedef struct rhp_http_compact {
+  int8_t   result;
+  uint8_t  body_kind;
+  uint8_t  flags;       /* RHP_HTTP_WIDE */
+  uint8_t  reserved;
+  uint32_t body_len;
+} rhp_http_compact_t;
+#define RHP_HTTP_WIDE 1u
+#define RHP_COMPACT_HTTP_WIDE_OFF(n) ((((size_t) (n) * 8u) + 15u) & ~(size_t) 15u)
+#define RHP_COMPACT_HTTP_BYTES(n) (RHP_COMPACT_HTTP_WIDE_OFF(n) + (size_t) (n) * 24u)
+
 typedef struct rhp_batch {
   const uint8_t  *bytes;   /* device, 16-byte aligned: packed requests + RHP_PAD zero bytes */
   uint8_t        *bytes_rw;/* device, RHP_MODE_HTTP: same buffer, writable (chunked
@@ -132,7 +154,8 @@ typedef struct rhp_batch {
   rhp_hdr_t      *hdrs;        /* device [n * max_headers] records, laid out as `layout` says
                                   (n * max_headers < 2^32); RHP_LAYOUT_COMPACT:
                                   RHP_COMPACT_HDRS_BYTES(n, max_headers) bytes */
-  rhp_http_t     *http;        /* device [n], RHP_MODE_HTTP */
+  rhp_http_t     *http;        /* device [n], RHP_MODE_HTTP (RHP_LAYOUT_COMPACT:
+                                  RHP_COMPACT_HTTP_BYTES(n) bytes, rhp_http_compact_t) */
   uint32_t       *work;        /* reserved, may be NULL (device scratch of RHP_WORK_WORDS u32
                                   for future kernels; the current ones keep their scheduling
                                   state in LDS) */

@@ -45,6 +45,10 @@ int rhp_emu_parse_batch(const rhp_batch_t *batch, uint64_t *stats);
  * records for RHP_F_WIDE requests).  `batch` supplies n, max_headers and
  * layout only.  0, or -22 on bad arguments. */
 int rhp_expand_records(const rhp_batch_t *batch, const rhp_req_t *reqs, const void *hdrs, rhp_hdr_t *out);
+/* A batch's http records (RHP_MODE_HTTP) as rhp_http_t[n]: copied, or for
+ * RHP_LAYOUT_COMPACT expanded from the compact records and their wide area
+ * (rhp.h rhp_http_compact_t; consumed from reqs[i].ret).  0, or -22. */
+int rhp_expand_http(const rhp_batch_t *batch, const rhp_req_t *reqs, const void *http, rhp_http_t *out);
 
 /* struct phr_header (picohttpparser.h:42-47): name == NULL for an obs-fold line */
 typedef struct rhp_phr_header {

@@ -64,7 +64,8 @@ RHP_SYMBOLS = ("rhp_parse_batch", "rhp_set_impl", "rhp_kernel_name", "rhp_versio
                "rhp_fixup_sessions")
 HOST_SYMBOLS = ("rhp_gen_size", "rhp_gen_fill", "rhp_gen_header_bytes", "rhp_splitmix64",
                 "rhp_emu_parse_batch", "rhp_cpu_parse_batch", "rhp_phr_parse_request", "rhp_http_read_cpu",
-                "rhp_cpu_fixup_sessions", "rhp_expand_records", "rhp_test_chunk_window", "rhp_test_chunk_exact")
+                "rhp_cpu_fixup_sessions", "rhp_expand_records", "rhp_expand_http", "rhp_test_chunk_window",
+                "rhp_test_chunk_exact")
 
 _rhp = None
 _host = None
@@ -128,6 +129,8 @@ def host() -> ctypes.CDLL:
         _host.rhp_cpu_fixup_sessions.restype = ctypes.c_int
         _host.rhp_expand_records.argtypes = [ctypes.POINTER(Batch), vp, vp, vp]
         _host.rhp_expand_records.restype = ctypes.c_int
+        _host.rhp_expand_http.argtypes = [ctypes.POINTER(Batch), vp, vp, vp]
+        _host.rhp_expand_http.restype = ctypes.c_int
     return _host
 
 
@@ -209,6 +212,7 @@ class Result:
     http: np.ndarray | None    # HTTP_DTYPE [n] (http mode)
     bytes_out: np.ndarray | None = None  # request bytes after http mode (chunked bodies rewritten)
     raw_hdrs: np.ndarray | None = None   # the hdrs buffer as the parser left it (its layout's bytes)
+    raw_http: np.ndarray | None = None   # the http buffer as the parser left it (compact: rhp_http_compact_t)
 
 
 def canonical(res: Result, mode: int):
@@ -269,6 +273,32 @@ def hdrs_bytes(n: int, max_headers: int, layout: int) -> int:
     return n * max_headers * HDR_DTYPE.itemsize
 
 
+def http_bytes(n: int, mode: int, layout: int) -> int:
+    """bytes the batch's http buffer needs (rhp.h; RHP_COMPACT_HTTP_BYTES for the compact layout)"""
+    if mode != MODE_HTTP:
+        return HTTP_DTYPE.itemsize
+    if layout == LAYOUT_COMPACT:
+        return ((n * 8 + 15) & ~15) + n * HTTP_DTYPE.itemsize
+    return n * HTTP_DTYPE.itemsize
+
+
+def expand_http(reqs: np.ndarray, raw: np.ndarray, n: int, layout: int) -> np.ndarray:
+    """[n] rhp_http_t records of a parsed http batch from its raw http bytes in any
+    layout (rhp_expand_http, include/rhp_host.h: compact records expanded)."""
+    raw = np.ascontiguousarray(raw).view(np.uint8)
+    if layout != LAYOUT_COMPACT:
+        return raw[: n * HTTP_DTYPE.itemsize].view(HTTP_DTYPE).copy()
+    out = np.zeros(n, dtype=HTTP_DTYPE)
+    if n == 0:
+        return out
+    reqs = np.ascontiguousarray(reqs)
+    b = Batch(None, None, None, 0, n, 0, MODE_HTTP, layout, None, None, None, None, 0, 0, None)
+    rc = host().rhp_expand_http(ctypes.byref(b), _ptr(reqs), _ptr(raw), _ptr(out))
+    if rc != 0:
+        raise RuntimeError(f"rhp_expand_http failed: {rc}")
+    return out
+
+
 def expand_records(reqs: np.ndarray, raw: np.ndarray, n: int, max_headers: int, layout: int) -> np.ndarray:
     """[n, max_headers] rhp_hdr_t records of a parsed batch from its raw hdrs bytes
     in any layout (rhp_expand_records, include/rhp_host.h): records of requests
@@ -296,19 +326,22 @@ def _host_batch(buf, off, max_headers, mode, layout=LAYOUT_REQUEST_MAJOR, last_l
     n = len(off) - 1
     reqs = np.zeros(n, dtype=REQ_DTYPE)
     raw = np.zeros(max(hdrs_bytes(n, max_headers, layout), 8), dtype=np.uint8)
-    http = np.zeros(n, dtype=HTTP_DTYPE)
+    raw_http = np.zeros(max(http_bytes(n, mode, layout), 8), dtype=np.uint8)
     rw = buf.copy()
     b = Batch(_ptr(rw), _ptr(rw), _ptr(off), rw.size, n, max_headers, mode, layout, _ptr(reqs), _ptr(raw),
-              _ptr(http), 0, flags, 0, _ptr(last_len) if last_len is not None else None)
+              _ptr(raw_http), 0, flags, 0, _ptr(last_len) if last_len is not None else None)
     hv = None if layout == LAYOUT_COMPACT else hdr_view(raw.view(HDR_DTYPE), n, max_headers, layout)
-    res = Result(reqs, hv, http if mode == MODE_HTTP else None, rw)
+    res = Result(reqs, hv, None, rw)
     res.raw_hdrs = raw   # the compact layout's records are expanded once the parse has run (_host_done)
+    res.raw_http = raw_http if mode == MODE_HTTP else None
     return b, res
 
 
 def _host_done(res: Result, n: int, max_headers: int, layout: int) -> Result:
     if layout == LAYOUT_COMPACT:
         res.hdrs = expand_records(res.reqs, res.raw_hdrs, n, max_headers, layout)
+    if res.raw_http is not None:
+        res.http = expand_http(res.reqs, res.raw_http, n, layout)
     return res
 
 
@@ -354,8 +387,7 @@ class DeviceBatch:
         self.offsets = torch.from_numpy(off.view(np.int64)).to(device)
         self.reqs = torch.zeros(self.n * REQ_DTYPE.itemsize, dtype=torch.uint8, device=device)
         self.hdrs = torch.zeros(max(hdrs_bytes(self.n, max_headers, layout), 8), dtype=torch.uint8, device=device)
-        self.http = torch.zeros((self.n if mode == MODE_HTTP else 1) * HTTP_DTYPE.itemsize, dtype=torch.uint8,
-                                device=device)
+        self.http = torch.zeros(http_bytes(self.n, mode, layout), dtype=torch.uint8, device=device)
         self.work = torch.zeros(RHP_WORK_WORDS, dtype=torch.int32, device=device)
         self.last_len = (torch.from_numpy(np.ascontiguousarray(last_len, dtype=np.uint64).view(np.int64)).to(device)
                          if last_len is not None else None)
@@ -381,9 +413,10 @@ class DeviceBatch:
         raw = self.hdrs.cpu().numpy()
         hdrs = (expand_records(reqs, raw, self.n, self.max_headers, self.layout) if self.layout == LAYOUT_COMPACT
                 else hdr_view(raw.view(HDR_DTYPE), self.n, self.max_headers, self.layout))
-        http = self.http.cpu().numpy().view(HTTP_DTYPE) if self.mode == MODE_HTTP else None
+        raw_http = self.http.cpu().numpy() if self.mode == MODE_HTTP else None
+        http = expand_http(reqs, raw_http, self.n, self.layout) if self.mode == MODE_HTTP else None
         out = self.bytes.cpu().numpy() if self.mode == MODE_HTTP else None
-        return Result(reqs, hdrs, http, out, raw)
+        return Result(reqs, hdrs, http, out, raw, raw_http)
 
 
 def parse_batch(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,
@@ -465,7 +498,7 @@ def fixup_cpu(buf, off, sessions, max_headers: int = 16, emulate_dfa: bool = Fal
     rc = host().rhp_cpu_fixup_sessions(ctypes.byref(b), _ptr(sessions), len(sessions), _ptr(out), _ptr(starts))
     if rc != 0:
         raise RuntimeError(f"rhp_cpu_fixup_sessions failed: {rc}")
-    return res, out, starts
+    return _host_done(res, len(off) - 1, max_headers, layout), out, starts
 
 
 def fixup_gpu(buf, off, sessions, max_headers: int = 16, impl: int = IMPL_DFA, layout: int = LAYOUT_REQUEST_MAJOR):

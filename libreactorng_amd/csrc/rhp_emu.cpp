@@ -45,6 +45,34 @@ rhp_hdr_t *wide_records(const rhp_batch_t *b, uint32_t i, uint64_t &hs_hdr)
   return b->hdrs + (uint64_t) i * (hmajor ? 1u : b->max_headers);
 }
 
+/* compact http records (rhp.h, RHP_LAYOUT_COMPACT in http mode): as the kernel,
+ * a record whose consumed follows from ret is stored compact, any other one
+ * (the exact path's, a chunked body de-framed in place) in the wide area */
+bool compact_http(const rhp_batch_t *b) { return b->mode == RHP_MODE_HTTP && b->layout == RHP_LAYOUT_COMPACT; }
+rhp_http_compact_t *http_compact(const rhp_batch_t *b) { return reinterpret_cast<rhp_http_compact_t *>(b->http); }
+rhp_http_t *http_wide(const rhp_batch_t *b)
+{
+  return reinterpret_cast<rhp_http_t *>(reinterpret_cast<uint8_t *>(b->http) + RHP_COMPACT_HTTP_WIDE_OFF(b->n));
+}
+void put_http(const rhp_batch_t *b, uint32_t i, const rhp_http_t &x, bool wide)
+{
+  if (!compact_http(b)) {
+    b->http[i] = x;
+    return;
+  }
+  rhp_http_compact_t c = {(int8_t) x.result, (uint8_t) x.body_kind, 0, 0, (uint32_t) x.body_len};
+  if (wide) {
+    c = rhp_http_compact_t{0, 0, (uint8_t) RHP_HTTP_WIDE, 0, 0};
+    http_wide(b)[i] = x;
+  }
+  http_compact(b)[i] = c;
+}
+/* the consumed a compact record stands for (rhp.h) */
+uint64_t compact_consumed(int32_t ret, const rhp_http_t &x)
+{
+  return x.result == 1 ? (uint64_t) ret + (x.body_kind == 1 ? x.body_len : 0u) : 0u;
+}
+
 void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
 {
   rhp_req_t r;
@@ -53,8 +81,9 @@ void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
   rhp_hdr_t *h = wide_records(b, i, hs_hdr);
   if (b->mode == RHP_MODE_HTTP) {
     PlainBytes B{b->bytes_rw + off};
-    scalar_http_t(B, b->bytes_rw + off, len, b->max_headers, &r, h, hs_hdr, &b->http[i],
-                  !(b->flags & RHP_BATCH_SPECULATIVE));
+    rhp_http_t x;
+    scalar_http_t(B, b->bytes_rw + off, len, b->max_headers, &r, h, hs_hdr, &x, !(b->flags & RHP_BATCH_SPECULATIVE));
+    put_http(b, i, x, true);
   }
   else {
     const uint64_t ll = b->last_len ? b->last_len[i] : 0;
@@ -75,7 +104,7 @@ void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
 
 extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] or NULL */)
 {
-  if (b->layout == RHP_LAYOUT_COMPACT && b->mode != RHP_MODE_PHR) return -22;   /* as rhp_parse_batch */
+  if (b->layout == RHP_LAYOUT_COMPACT && (b->flags & RHP_BATCH_SPECULATIVE)) return -22;   /* as rhp_parse_batch */
   const Table2 &T = table();
   const uint8_t *cls = T.b + kClassRow * 256u;
   Stats st_count = {0, 0, 0};
@@ -168,8 +197,22 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
         r.num_headers = (uint16_t) d.nh;
         r.flags = 0;
         b->reqs[i] = r;
-        if (b->mode == RHP_MODE_HTTP)
-          http_frame(b->bytes_rw + off, len, r, hout, hs_hdr, &b->http[i], ~0ull, !(b->flags & RHP_BATCH_SPECULATIVE));
+        if (b->mode == RHP_MODE_HTTP) {
+          rhp_http_t x;
+          if (compact) {   /* http_frame reads rhp_hdr_t records: the lengths expanded */
+            rhp_hdr_t tmp[RHP_MAX_HEADERS];
+            uint32_t at = (uint32_t) r.path_off + r.path_len + 11u;
+            for (uint32_t k = 0; k < d.nh && k < maxh; k++) {
+              const uint32_t l = lens[(uint64_t) k * b->n], nl = l & 0xffffu, vl = l >> 16;
+              tmp[k] = rhp_hdr_t{(uint16_t) at, (uint16_t) nl, (uint16_t) (at + nl + 2u), (uint16_t) vl};
+              at += nl + vl + 4u;
+            }
+            http_frame(b->bytes_rw + off, len, r, tmp, 1u, &x, ~0ull, !(b->flags & RHP_BATCH_SPECULATIVE));
+          } else {
+            http_frame(b->bytes_rw + off, len, r, hout, hs_hdr, &x, ~0ull, !(b->flags & RHP_BATCH_SPECULATIVE));
+          }
+          put_http(b, i, x, x.consumed != compact_consumed(r.ret, x) || x.body_len > 0xffffffffull);
+        }
       } else if (bad) {
         st_count.fast_bad++;
         rhp_req_t r;
@@ -178,8 +221,10 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
         r.minor_version = -1;
         b->reqs[i] = r;
         if (b->mode == RHP_MODE_HTTP) {
-          memset(&b->http[i], 0, sizeof b->http[i]);
-          b->http[i].result = -1;
+          rhp_http_t x;
+          memset(&x, 0, sizeof x);
+          x.result = -1;
+          put_http(b, i, x, false);
         }
       } else {
         st_count.exact++;
@@ -241,6 +286,27 @@ extern "C" int rhp_expand_records(const rhp_batch_t *b, const rhp_req_t *reqs, c
       for (uint32_t k = 0; k < nh; k++)
         o[k] = compact ? wide[(uint64_t) i * m + k] : hmajor ? h[(uint64_t) k * n + i] : h[(uint64_t) i * m + k];
     }
+  }
+  return 0;
+}
+
+extern "C" int rhp_expand_http(const rhp_batch_t *b, const rhp_req_t *reqs, const void *http, rhp_http_t *out)
+{
+  if (!b || !reqs || !http || !out) return -22;
+  if (b->layout != RHP_LAYOUT_COMPACT) {
+    memcpy(out, http, sizeof(rhp_http_t) * b->n);
+    return 0;
+  }
+  const rhp_http_compact_t *c = static_cast<const rhp_http_compact_t *>(http);
+  const rhp_http_t *wide = reinterpret_cast<const rhp_http_t *>(static_cast<const uint8_t *>(http) + RHP_COMPACT_HTTP_WIDE_OFF(b->n));
+  for (uint32_t i = 0; i < b->n; i++) {
+    if (c[i].flags & RHP_HTTP_WIDE) {
+      out[i] = wide[i];
+      continue;
+    }
+    rhp_http_t x = {c[i].result, c[i].body_kind, 0, c[i].body_len};
+    x.consumed = compact_consumed(reqs[i].ret, x);
+    out[i] = x;
   }
   return 0;
 }

@@ -34,6 +34,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <atomic>
+#include <type_traits>
 
 #include "rhp.h"
 #include "rhp_dfa.h"
@@ -68,7 +69,30 @@ struct Params {
   uint32_t *lens;
   uint32_t rec_req, rec_hdr;
   bool wt_records;   /* records header-major or compact in phr mode: write-through where a range is even */
+  /* RHP_LAYOUT_COMPACT in http mode: the 8-byte http records (rhp.h
+   * rhp_http_compact_t); `http` then points at their wide area, which also
+   * holds the replay's hints */
+  uint2 *hc;
 };
+
+/* http records (RHP_MODE_HTTP).  With compact records (p.hc) a record whose
+ * consumed follows from ret (rhp.h) is stored compact; the wide ones (the exact
+ * path, chunked bodies) go to the wide area and the compact record says so. */
+__device__ __forceinline__ void store_hc(const Params &p, uint32_t i, uint32_t w0, uint32_t w1)
+{
+  typedef uint32_t u32x2a8 __attribute__((ext_vector_type(2), aligned(8)));
+  *((__attribute__((address_space(1))) u32x2a8 *) (p.hc + i)) = u32x2a8{w0, w1};
+}
+__device__ __forceinline__ void mark_wide(const Params &p, uint32_t i)
+{
+  if (p.hc) store_hc(p, i, RHP_HTTP_WIDE << 16, 0u);
+}
+/* a final record whose consumed is ret (+ body_len for a Content-Length body), or 0 */
+__device__ __forceinline__ void put_http(const Params &p, uint32_t i, const rhp_http_t &o)
+{
+  if (p.hc) store_hc(p, i, ((uint32_t) o.result & 0xffu) | o.body_kind << 8, (uint32_t) o.body_len);
+  else p.http[i] = o;
+}
 
 #ifndef RHP_WAVES_PER_SIMD
 #define RHP_WAVES_PER_SIMD 4
@@ -385,6 +409,7 @@ __device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64
     LineBytes B{p.bytes_rw + off, ~0ull, {0, 0, 0, 0}};
     scalar_http_t(B, p.bytes_rw + off, len, p.max_headers, &r, h, p.hs_hdr, &x, p.compact, DevDechunk{});
     p.http[i] = x;
+    mark_wide(p, i);
   } else {
     LineBytes B{p.bytes + off, ~0ull, {0, 0, 0, 0}};
     const uint64_t ll = p.last_len ? p.last_len[i] : 0;
@@ -465,9 +490,9 @@ __device__ __forceinline__ uint64_t strtoull10_gpu(const uint8_t *s, const uint3
  * traffic.  The candidates' names and values are loaded together, one memory
  * round trip. */
 enum : int { kFrameDone = 0, kFrameSlow = 1, kFrameChunked = 2 };
-__device__ __forceinline__ int http_frame_fast(const uint8_t *b, uint64_t len, int32_t ret, rhp_http_t *x,
-                                               uint32_t cand, uint32_t crec_lo, uint32_t crec_hi,
-                                               const rhp_hdr_t *h, uint64_t hs)
+template <class Rec>
+__device__ __forceinline__ int http_frame_fast(const uint8_t *b, uint64_t len, int32_t ret, rhp_http_t &x,
+                                               uint32_t cand, uint32_t crec_lo, uint32_t crec_hi, Rec &&rec)
 {
   const int64_t n = ret;
   rhp_http_t o = {1, 0, (uint64_t) n, 0};
@@ -481,7 +506,7 @@ __device__ __forceinline__ int http_frame_fast(const uint8_t *b, uint64_t len, i
      * (its length is 14 or 17). */
     uint32_t lo[2] = {crec_lo, 0u}, hi[2] = {crec_hi, 0u};
     if (rest) {
-      const uint2 r = *reinterpret_cast<const uint2 *>(h + (uint64_t) __builtin_ctz(rest) * hs);
+      const uint2 r = rec((uint32_t) __builtin_ctz(rest));   /* record of header index j (the second candidate) */
       lo[1] = r.x; hi[1] = r.y;
     }
     uint32_t dn[2][7], dv[2][7];
@@ -527,7 +552,7 @@ __device__ __forceinline__ int http_frame_fast(const uint8_t *b, uint64_t len, i
       }
     }
   }
-  *x = o;
+  x = o;
   return kFrameDone;
 }
 
@@ -1063,6 +1088,17 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   /* the extension parts of the wave's windows (kXParts > 0): after the pool area */
   const uint32_t xstage = __builtin_amdgcn_readfirstlane(kLdsTable + WAVES * kStageWave + kPoolBytes +
                                                          (tid >> 6) * 1024u * kXParts);
+  /* the first window of the request starting at (low dword) o0: its 4-aligned
+   * start, offset from base.  RHP_DIAG_LINE_WINDOWS (diagnostic build, wrong
+   * records): the 128-byte line holding it, as line-aligned windows would
+   * fetch, for the traffic and time such windows cost */
+  auto first_win = [&](uint32_t o0) -> uint32_t {
+#ifdef RHP_DIAG_LINE_WINDOWS
+    const uint32_t l = (o0 & ~127u) - (uint32_t) base;
+    if ((o0 & ~127u) - (uint32_t) base <= (o0 & ~3u) - (uint32_t) base) return l;
+#endif
+    return (o0 & ~3u) - (uint32_t) base;
+  };
   /* LDS address of part q of this lane's window */
   auto part_lds = [&](uint32_t q) -> uint32_t {
     return q < kParts ? stage + stage_off(lane, q) : xstage + 1024u * (q - kParts) + 16u * lane;
@@ -1226,10 +1262,50 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     uint32_t com = t ? m ^ odd : odd;    /* t = 1: the word opens with an EOL */
     uint32_t eolm = m ^ com;
     if (!__builtin_amdgcn_ballot_w64(nh + (uint32_t) __builtin_popcount(eolm) >= maxh)) {
-      /* no lane can reach max_headers in this word: no capacity checks */
-      /* Straight-line body for every lane (a masked `if` costs more in copies
-       * than it saves): a lane whose word is done (eolm == 0) computes a dead
-       * record, stores nothing and keeps its state */
+      /* no lane can reach max_headers in this word: no capacity checks.  The
+       * lanes with a record in the word loop over their records under exec
+       * (a lane leaves the loop after its last record), one record per trip;
+       * the store flavour is chosen outside the loop */
+#ifndef RHP_DECODE_SELECT
+      if (eolm != 0) {
+        auto records = [&](auto wt_c) __attribute__((always_inline)) {
+          do {
+            const uint32_t e = base + (uint32_t) __builtin_ctz(eolm);
+            const uint32_t co = t ? pco : base + (uint32_t) __builtin_ctz(com | 0x80000000u);
+            com = t ? com : com & (com - 1u);
+            eolm &= eolm - 1u;
+            const uint32_t nlen = co - ls, vlen = e - co - 3u;
+            if constexpr (COMPACT) {
+              uint32_t *q = p.lens + hx;
+              if constexpr (decltype(wt_c)::value)
+                asm volatile("global_store_dword %0, %1, off sc1" ::"v"(q), "v"(nlen | vlen << 16) : "memory");
+              else *GLOBAL(uint32_t, q) = nlen | vlen << 16;
+            } else {
+              rhp_hdr_t *q = p.hdrs + hx;
+              const u32x2 v = u32x2{ls | nlen << 16, (co + 2u) | vlen << 16};
+              if constexpr (decltype(wt_c)::value)
+                asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(q), "v"(v) : "memory");
+              else *GLOBAL(u32x2, q) = v;
+            }
+            if (http) {   /* uniform: framing candidates only in http mode */
+              const bool cnd = nlen == 14u || nlen == 17u;
+              const bool first = cnd && (cand & 0xbfffffffu) == 0;
+              crec_lo = first ? ls | nlen << 16 : crec_lo;
+              crec_hi = first ? (co + 2u) | vlen << 16 : crec_hi;
+              cand |= cnd ? (nh < 30u ? 1u << nh : 0x80000000u) : 0u;
+            }
+            ls = e + 1u;
+            nh++;
+            hx += p.rec_hdr;
+            t = 0;
+          } while (eolm != 0);
+        };
+        if (wt) records(std::true_type{});
+        else records(std::false_type{});
+      }
+#else
+      /* Straight-line body for every lane: a lane whose word is done (eolm ==
+       * 0) computes a dead record, stores nothing and keeps its state */
       while (uint64_t st_m = __builtin_amdgcn_ballot_w64(eolm != 0)) {
         const bool has = eolm != 0;
         const uint32_t e = base + (uint32_t) __builtin_ctz(eolm | 0x80000000u);
@@ -1252,6 +1328,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         hx += has ? p.rec_hdr : 0u;
         t = has ? 0u : t;
       }
+#endif
       /* a colon left open at the end of the word: a later word (or window) has its LF */
       if (com) {
         pco = base + (uint32_t) __builtin_ctz(com);
@@ -1510,7 +1587,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
                 x.body_kind = 1; x.body_len = size; x.consumed = (uint64_t) ret + size;
               }
             }
-            store_http(p.http + dcur, x);
+            if constexpr (COMPACT) store_hc(p, dcur, ((uint32_t) x.result & 0xffu) | x.body_kind << 8, (uint32_t) x.body_len);
+            else store_http(p.http + dcur, x);
             framed = true;
           }
         }
@@ -1528,7 +1606,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       }
     } else if (bad) {
       rq[0] = 0xffffffffu;   /* -1 */
-      if (http) store_http_bad(p.http + dcur);
+      if (http) {
+        if constexpr (COMPACT) store_hc(p, dcur, 0xffu, 0u);   /* result -1 */
+        else store_http_bad(p.http + dcur);
+      }
     } else {
       rq[3] = (uint32_t) kDeferExact << 16;   /* exact path: replay */
       defer(dcur);
@@ -1673,13 +1754,13 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     if (!idle_wave) {
       refill_pend();
       wait_vm0();
-      nw = pend_ok ? ((pend_o0 & ~3u) - (uint32_t) base) | 2u : 0u;
+      nw = pend_ok ? first_win(pend_o0) | 2u : 0u;
       issue();
     }
   } else {
     /* the first windows, then the barrier that makes the pool area
      * initialized before any wave's first refill */
-    nw = pend_ok ? ((pend_o0 & ~3u) - (uint32_t) base) | 2u : 0u;
+    nw = pend_ok ? first_win(pend_o0) | 2u : 0u;
     issue();
     __syncthreads();
   }
@@ -1762,7 +1843,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       /* [E] next window: continuation of wcur, else the first window of a ready pend */
       nw = 0;
       if (walking && (uint32_t) (wpos + (int32_t) kWBlock) < wlen) nw = (cur_ptr + kWBlock) | 1u;
-      else if (pend_ready) nw = ((p_o0 & ~3u) - (uint32_t) base) | 2u;
+      else if (pend_ready) nw = first_win(p_o0) | 2u;
       wait_lgkm0();   /* [A]'s reads of the buffer are done */
       issue();
       dg.section(1, true);
@@ -1824,7 +1905,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       /* [E] (the decode above read the staging buffer the issue refills) */
       nw = 0;
       if (walking && wact) nw = (cur_ptr + kWBlock) | 1u;
-      else if (pend_ok) nw = ((pend_o0 & ~3u) - (uint32_t) base) | 2u;
+      else if (pend_ok) nw = first_win(pend_o0) | 2u;
       wait_lgkm0();
       issue();
     }
@@ -1913,13 +1994,34 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
      * its http record still holds the hint */
     auto finish_slow = [&](uint32_t i, const Head &h) {
       const uint32_t f = what(h);
-      if (f & kHintExact) {
+      if ((f & kHintExact) || p.hc) {   /* compact records: http_frame has no rhp_hdr_t to read, the exact path frames */
         finish_exact(p, i, h.off, h.end - h.off);
       } else {
         const uint32_t cand = h.hint[0];
         http_frame(p.bytes_rw + h.off, h.end - h.off, p.reqs[i], p.hdrs + (uint64_t) i * p.hs_req, p.hs_hdr,
                    &p.http[i], (cand >> 31) ? ~0ull : (uint64_t) (cand & 0x3fffffffu), p.compact, DevDechunk{});
       }
+    };
+    /* http_frame_fast from request i's hint; its record stored when it settles
+     * the request.  The second candidate's record (index j): from hdrs, or, in
+     * the compact layout, summed from the lengths after the first one's */
+    auto frame_fast = [&](uint32_t i, const Head &h) {
+      const uint32_t cand = h.hint[0], crec_hi = h.hint[3];
+      auto rec = [&](uint32_t j) -> uint2 {
+        if (!p.hc) return *reinterpret_cast<const uint2 *>(p.hdrs + (uint64_t) i * p.hs_req + (uint64_t) j * p.hs_hdr);
+        uint32_t at = (crec_hi & 0xffffu) + (crec_hi >> 16) + 2u;   /* the line after the first candidate's */
+        for (uint32_t k = (uint32_t) __builtin_ctz(cand & 0x3fffffffu) + 1u; k < j; k++) {
+          const uint32_t l = p.lens[(uint64_t) k * p.rec_hdr + i];
+          at += (l & 0xffffu) + (l >> 16) + 4u;
+        }
+        const uint32_t l = p.lens[(uint64_t) j * p.rec_hdr + i];
+        return uint2{at | (l & 0xffffu) << 16, (at + (l & 0xffffu) + 2u) | (l >> 16) << 16};
+      };
+      rhp_http_t o;
+      const int fr = http_frame_fast(p.bytes_rw + h.off, h.end - h.off, (int32_t) (h.hint[1] & 0xffffu), o, cand,
+                                     h.hint[2], crec_hi, rec);
+      if (fr == kFrameDone) put_http(p, i, o);
+      return fr;
     };
     /* the list lives where the DFA table was (idle now); the staging area
      * holds the chunked bodies' LDS slots (staged_moves) */
@@ -1949,17 +2051,16 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (!f) continue;
       const int fr = (f & kHintExact)                 ? kFrameSlow
                      : (cur.hint[1] & kHintChunked) ? kFrameChunked   /* settled in the loop */
-                                                    : http_frame_fast(p.bytes_rw + cur.off, cur.end - cur.off,
-                                                        (int32_t) (cur.hint[1] & 0xffffu), &p.http[i], cur.hint[0],
-                                                        cur.hint[2], cur.hint[3], p.hdrs + (uint64_t) i * p.hs_req, p.hs_hdr);
+                                                    : frame_fast(i, cur);
       dg.framed(fr == kFrameDone);
       if (fr != kFrameDone) {
         /* listed: the range-relative index, bit 31 = a chunked body to de-frame */
         const uint32_t at = atomicAdd(slow_n, 1u);
         if (at < kSlowCap) slow[at] = (i - wg_lo) | (fr == kFrameChunked ? 0x80000000u : 0u);
-        else if (fr == kFrameChunked)   /* list full (a range of > kSlowCap such requests) */
+        else if (fr == kFrameChunked) {   /* list full (a range of > kSlowCap such requests) */
           frame_chunked(p.bytes_rw + cur.off, cur.end - cur.off, (int32_t) (cur.hint[1] & 0xffffu), &p.http[i], p.compact);
-        else finish_slow(i, cur);
+          mark_wide(p, i);
+        } else finish_slow(i, cur);
       }
     }
     dg.pass_end(1);
@@ -1989,9 +2090,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
           const int fr = !f                              ? kFrameDone
                          : (f & kHintExact)              ? kFrameSlow
                          : (h.hint[1] & kHintChunked)    ? kFrameChunked
-                                                         : http_frame_fast(p.bytes_rw + h.off, h.end - h.off,
-                                                             (int32_t) (h.hint[1] & 0xffffu), &p.http[i], h.hint[0],
-                                                             h.hint[2], h.hint[3], p.hdrs + (uint64_t) i * p.hs_req, p.hs_hdr);
+                                                         : frame_fast(i, h);
           e = fr == kFrameDone ? 0x40000000u : fr == kFrameChunked ? 0x80000000u : 0u;
         } else {
           e = slow[k];
@@ -2020,6 +2119,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         while (__builtin_amdgcn_ballot_w64(w.live)) w.step();   /* what the last round's moves left */
         StagedBody sb;
         const bool staged = walking && finish_chunked(w, wret, &p.http[wi], p.compact, &sb);
+        if (walking) mark_wide(p, wi);
         dg.part_end(4);
         const uint64_t m = __builtin_amdgcn_ballot_w64(staged);
         if (kb + WAVES * 64 < ns) start_round(kb + WAVES * 64);
@@ -2151,7 +2251,7 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   if (b->mode == RHP_MODE_HTTP && (!b->http || !b->bytes_rw)) return -22;
   if (b->mode != RHP_MODE_PHR && b->mode != RHP_MODE_HTTP) return -22;
   if (b->layout != RHP_LAYOUT_REQUEST_MAJOR && b->layout != RHP_LAYOUT_HEADER_MAJOR &&
-      !(b->layout == RHP_LAYOUT_COMPACT && b->mode == RHP_MODE_PHR)) return -22;   /* compact: phr mode */
+      !(b->layout == RHP_LAYOUT_COMPACT && !(b->flags & RHP_BATCH_SPECULATIVE))) return -22;   /* compact: not speculative */
   if (b->last_len && b->mode != RHP_MODE_PHR) return -22;   /* http_read_request passes last_len 0 */
   if ((b->flags & ~RHP_BATCH_SPECULATIVE) || ((b->flags & RHP_BATCH_SPECULATIVE) && b->mode != RHP_MODE_HTTP)) return -22;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -2182,6 +2282,7 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.hs_req = hmajor ? 1u : b->max_headers;
   prm.hs_hdr = hmajor ? b->n : 1u;
   prm.lens = nullptr;
+  prm.hc = nullptr;
   prm.rec_req = prm.hs_req;
   prm.rec_hdr = prm.hs_hdr;
   prm.wt_records = b->mode == RHP_MODE_PHR && b->layout != RHP_LAYOUT_REQUEST_MAJOR;
@@ -2190,6 +2291,10 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
     prm.hdrs = reinterpret_cast<rhp_hdr_t *>(reinterpret_cast<uint8_t *>(b->hdrs) + RHP_COMPACT_WIDE_OFF(b->n, b->max_headers));
     prm.rec_req = 1u;
     prm.rec_hdr = b->n;
+    if (b->mode == RHP_MODE_HTTP) {   /* 8-byte http records, the wide ones (and the replay's hints) behind them */
+      prm.hc = reinterpret_cast<uint2 *>(b->http);
+      prm.http = reinterpret_cast<rhp_http_t *>(reinterpret_cast<uint8_t *>(b->http) + RHP_COMPACT_HTTP_WIDE_OFF(b->n));
+    }
   }
 
   /* the DFA kernel addresses windows with u32 offsets from its workgroup's
@@ -2201,7 +2306,8 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
     return (int) hipGetLastError();
   }
   const bool late = late_issue(b->mode);
-  if (b->mode == RHP_MODE_HTTP) return launch_dfa<kHttpWaves, true, true, false>(prm, s, dev, cus);
+  if (b->mode == RHP_MODE_HTTP)
+    return compact ? launch_dfa<kHttpWaves, true, true, true>(prm, s, dev, cus) : launch_dfa<kHttpWaves, true, true, false>(prm, s, dev, cus);
   if (compact) return late ? launch_dfa<16, true, false, true>(prm, s, dev, cus) : launch_dfa<16, false, false, true>(prm, s, dev, cus);
   if (late) return launch_dfa<16, true, false, false>(prm, s, dev, cus);
   return launch_dfa<16, false, false, false>(prm, s, dev, cus);

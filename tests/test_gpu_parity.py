@@ -36,10 +36,6 @@ def golden(name):
 @pytest.mark.parametrize("name", sorted(MANIFEST))
 def test_gpu_matches_reference_golden(name, impl, layout):
     spec, buf, off, want, z = golden(name)
-    if layout == rhp.LAYOUT_COMPACT and spec["mode"] != rhp.MODE_PHR:
-        with pytest.raises(RuntimeError):   # the compact records are a phr-mode layout (rhp.h): -22
-            rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], impl=impl, layout=layout)
-        return
     res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], impl=impl, layout=layout)
     assert_same(canon(res, spec["mode"]), want, buf, off, f"GPU impl{impl} vs golden {name}")
     if "bytes_out_sha256" in z.files:
@@ -62,16 +58,23 @@ def test_gpu_compact_fuzz_vs_oracle(maxh):
     """Compact records (RHP_LAYOUT_COMPACT): lengths from the DFA, wide records
     from the exact path (RHP_F_WIDE) exactly where the emulator takes it; the
     expanded records equal the oracle's."""
-    for impl, seed in ((rhp.IMPL_DFA, 9300 + maxh), (rhp.IMPL_DFA_LATE, 9400 + maxh)):
-        buf, off = rhp.generate(rhp.GEN_FUZZ, 60000, seed)
-        res = rhp.parse_batch(buf, off, maxh, rhp.MODE_PHR, impl=impl, layout=rhp.LAYOUT_COMPACT)
-        want = to_rhp(*run_oracle(buf, off, maxh, rhp.MODE_PHR)[:3], rhp.MODE_PHR)
-        assert_same(canon(res, rhp.MODE_PHR), want, buf, off, f"GPU compact fuzz impl{impl} maxh{maxh}")
-        emu, _ = rhp.emulate(buf, off, maxh, rhp.MODE_PHR, rhp.LAYOUT_COMPACT)
+    for cfg, mode, impl, seed in ((rhp.GEN_FUZZ, rhp.MODE_PHR, rhp.IMPL_DFA, 9300 + maxh),
+                                  (rhp.GEN_FUZZ, rhp.MODE_PHR, rhp.IMPL_DFA_LATE, 9400 + maxh),
+                                  (rhp.GEN_FUZZ_HTTP, rhp.MODE_HTTP, rhp.IMPL_DFA, 9500 + maxh)):
+        buf, off = rhp.generate(cfg, 60000, seed)
+        res = rhp.parse_batch(buf, off, maxh, mode, impl=impl, layout=rhp.LAYOUT_COMPACT)
+        want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
+        assert_same(canon(res, mode), want, buf, off, f"GPU compact fuzz cfg{cfg} impl{impl} maxh{maxh}")
+        emu, _ = rhp.emulate(buf, off, maxh, mode, rhp.LAYOUT_COMPACT)
         assert np.array_equal(res.reqs["flags"] & (rhp.F_EXACT | rhp.F_WIDE), emu.reqs["flags"] & (rhp.F_EXACT | rhp.F_WIDE))
+        if mode == rhp.MODE_HTTP:   # de-framed bytes too; exact-path http records are wide
+            assert (res.bytes_out == run_oracle(buf, off, maxh, mode)[3]).all()
+            wide = (res.raw_http[:8 * len(res.reqs)].reshape(-1, 8)[:, 2] & 1) != 0
+            assert wide[(res.reqs["flags"] & rhp.F_EXACT) != 0].all()
 
 
-@pytest.mark.parametrize("name", ["config2_get256_h16", "config3_zipf_h32", "config4_get256_shard5of8"])
+@pytest.mark.parametrize("name", ["config2_get256_h16", "config3_zipf_h32", "config4_get256_shard5of8",
+                                  "config5_post1k_http_h16", "chunked_post_http_h16"])
 def test_gpu_compact_full_size_matches_reference_digest(name):
     spec = FULL[name]
     buf, off = inputs(spec)
@@ -81,6 +84,8 @@ def test_gpu_compact_full_size_matches_reference_digest(name):
         want = to_rhp(*run_oracle(buf, off, spec["max_headers"], spec["mode"])[:3], spec["mode"])
         assert_same(got, want, buf, off, name)
         raise AssertionError(f"{name}: compact digest differs from the reference but matches the oracle")
+    if "bytes_out_sha256" in spec:
+        assert hashlib.sha256(res.bytes_out.tobytes()).hexdigest() == spec["bytes_out_sha256"]
 
 
 @pytest.mark.parametrize("maxh", [0, 1, 3, 16, 32, 64])
@@ -103,9 +108,10 @@ def test_gpu_edge_cases(shift):
     buf, off = pack(EDGE * 3, align_shift=shift)
     for maxh in (0, 1, 16):
         for mode in (rhp.MODE_PHR, rhp.MODE_HTTP):
-            res = rhp.parse_batch(buf, off, maxh, mode)
             want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
-            assert_same(canon(res, mode), want, buf, off, f"GPU edge shift{shift} maxh{maxh} mode{mode}")
+            for layout in (rhp.LAYOUT_REQUEST_MAJOR, rhp.LAYOUT_COMPACT):
+                res = rhp.parse_batch(buf, off, maxh, mode, layout=layout)
+                assert_same(canon(res, mode), want, buf, off, f"GPU edge shift{shift} maxh{maxh} mode{mode} layout{layout}")
 
 
 def test_gpu_toolong_and_empty_batch():

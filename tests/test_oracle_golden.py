@@ -39,12 +39,17 @@ def test_oracle_matches_reference_golden(name):
 @pytest.mark.parametrize("name", sorted(SETS))
 def test_dfa_emulation_matches_golden(name, layout):
     spec, buf, off, want, z = load_golden(name)
-    if layout == rhp.LAYOUT_COMPACT and spec["mode"] != rhp.MODE_PHR:
-        with pytest.raises(RuntimeError):   # compact records: phr mode only (rhp.h)
-            rhp.emulate(buf, off, spec["max_headers"], spec["mode"], layout)
-        return
     res, stats = rhp.emulate(buf, off, spec["max_headers"], spec["mode"], layout)
     assert_same(canon(res, spec["mode"]), want, buf, off, f"DFA emulation vs golden {name}")
+    if layout == rhp.LAYOUT_COMPACT and spec["mode"] == rhp.MODE_HTTP:
+        # compact http records (rhp.h rhp_http_compact_t): the DFA-framed requests are stored
+        # compact, only the exact path's and de-framed chunked bodies' records are wide
+        flags = res.raw_http[:8 * len(res.reqs)].reshape(-1, 8)[:, 2]
+        wide = (flags & 1) != 0
+        dfa = (res.reqs["flags"] & 1) == 0
+        assert wide[~dfa].all(), "exact-path records are wide"
+        if name.startswith("config5"):   # Content-Length POSTs: framed in the DFA path
+            assert (~wide[dfa]).mean() > 0.9, "DFA-framed records are compact"
     if "bytes_out_sha256" in z.files:
         assert hashlib.sha256(res.bytes_out.tobytes()).digest() == z["bytes_out_sha256"].tobytes()
 

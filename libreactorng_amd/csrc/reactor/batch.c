@@ -562,17 +562,43 @@ void reactor_batch_result(int k, reactor_batch_result_t *out)
     /* only the records came back (reactor_batch_submit): the bytes, de-framed
      * in place by the fix-up, are fetched when some request of the round has a
      * chunked body (the server copies that body from them, server.c) */
-    bool chunked = false;
-    for (uint32_t i = 0; i < s->n && !chunked; i++)
+    /* only the requests whose chunked body was de-framed: their byte ranges
+     * [req_start, + consumed), adjacent ones merged into one copy, or the span
+     * from the first to the last when they are many (the whole
+     * input came back for one such request) */
+    enum { MAX_RUNS = 16 };
+    uint64_t run_lo[MAX_RUNS], run_hi[MAX_RUNS], span_lo = 0, span_hi = 0;
+    uint32_t runs = 0;
+    for (uint32_t i = 0; i < s->n; i++)
     {
       const rhp_http_t *x = &s->h_http[i];
-      chunked = x->result == 1 && x->body_kind && x->consumed != (uint64_t) s->h_req[i].ret + x->body_len;
+      if (!(x->result == 1 && x->body_kind && x->consumed != (uint64_t) s->h_req[i].ret + x->body_len))
+        continue;
+      const uint64_t a = s->h_start[i], b = a + x->consumed;
+      span_lo = runs && span_lo < a ? span_lo : a;
+      span_hi = b > span_hi ? b : span_hi;
+      if (runs && runs <= MAX_RUNS && a <= run_hi[runs - 1])
+        run_hi[runs - 1] = b > run_hi[runs - 1] ? b : run_hi[runs - 1];
+      else
+      {
+        if (runs < MAX_RUNS)
+        {
+          run_lo[runs] = a;
+          run_hi[runs] = b;
+        }
+        runs++;
+      }
     }
-    if (chunked)
+    if (runs)
     {
       if (!B->cstream)
         HIP(hipStreamCreateWithFlags(&B->cstream, hipStreamNonBlocking));
-      HIP(hipMemcpyAsync(s->h_buf, s->d_buf, s->bytes, hipMemcpyDeviceToHost, B->cstream));
+      if (runs > MAX_RUNS)
+        HIP(hipMemcpyAsync(s->h_buf + span_lo, s->d_buf + span_lo, span_hi - span_lo, hipMemcpyDeviceToHost, B->cstream));
+      else
+        for (uint32_t r = 0; r < runs; r++)
+          HIP(hipMemcpyAsync(s->h_buf + run_lo[r], s->d_buf + run_lo[r], run_hi[r] - run_lo[r], hipMemcpyDeviceToHost,
+                             B->cstream));
       HIP(hipStreamSynchronize(B->cstream));
     }
   }

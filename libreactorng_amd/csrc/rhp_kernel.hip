@@ -143,6 +143,15 @@ static_assert(idx2(S_DONE, 0) == kPark, "parked lanes sit in DONE");
  * the kernel's window geometry) and the waves its staging leaves room for */
 constexpr uint32_t kHttpXParts = RHP_HTTP_XPARTS;   /* rhp_dfa.h: the emulator walks the same windows */
 constexpr int kHttpWaves = kHttpXParts == 0 ? 16 : kHttpXParts <= 2 ? 12 : 8;
+/* the lowest pair index of a state that is not terminal (DONE, ERR, SLOW and
+ * their event forms are the indices below it) */
+constexpr uint32_t kLiveIdx = idx2(S_SLOW, 1) + 1u;
+static_assert(idx2(S_DONE, 0) < kLiveIdx && idx2(S_ERR, 1) < kLiveIdx && idx2(S_DONE_E, 3) < kLiveIdx &&
+              idx2(S_ERR_E, 3) < kLiveIdx && idx2(S_SKIP3, 0) >= kLiveIdx && idx2(S_SP1_E, 2) >= kLiveIdx,
+              "terminal indices lie below every live one");
+#ifndef RHP_PHASE_LOCK
+#define RHP_PHASE_LOCK 1
+#endif
 
 /* LDS byte address of part q (16 B) of lane w's window inside the staging
  * buffer.  The LDS-DMA loads of a wave write lane-linearly (1 KiB per
@@ -1013,6 +1022,16 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * iterations saved) and no fewer bytes fetched (the 32 B of the next line
    * cost its whole line), so the default is 0. */
   constexpr uint32_t kXParts = (LATE && HTTP) ? kHttpXParts : 0u;
+  /* Phase lock (http form, RHP_PHASE_LOCK): a lane walks the first window of a
+   * request only on even iterations.  Header sections of one or two windows
+   * (config 5: 133 B) then keep every lane of a wave in step -- first windows on
+   * even iterations, second windows on odd ones -- and on an odd iteration
+   * every lane reaches its terminal within the window's first parts, where the
+   * walk stops (walk()).  A lane whose request ended in its first window idles
+   * one iteration; without the lock the lanes drift out of step after the
+   * first such request and no walk ever stops early. */
+  constexpr bool kPhaseLock = RHP_PHASE_LOCK && LATE && HTTP;
+  uint32_t it_odd = 0;   /* wave-uniform: this iteration's number is odd */
   constexpr uint32_t kWParts = kParts + kXParts;   /* 16-byte parts per window */
   constexpr uint32_t kWBlock = 16u * kWParts;      /* window bytes */
   constexpr uint32_t kWEv = kWBlock / 32u;         /* 32-bit event words per window */
@@ -1667,6 +1686,12 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #pragma unroll
         for (int j = 0; j < 8; j++) c[j] = cn[j];
       }
+      /* phase-locked http form: once every lane of the wave is terminal (or
+       * parked) the rest of the window changes nothing -- terminal states are
+       * absorbing and fire no event -- so the walk stops at the end of an event
+       * word (q odd: the word holds its 16 steps) */
+      if constexpr (kPhaseLock)
+        if ((q & 1) && nx && !__builtin_amdgcn_ballot_w64(st >= kLiveIdx)) break;
     }
   };
 
@@ -1905,7 +1930,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       /* [E] (the decode above read the staging buffer the issue refills) */
       nw = 0;
       if (walking && wact) nw = (cur_ptr + kWBlock) | 1u;
-      else if (pend_ok) nw = first_win(pend_o0) | 2u;
+      else if (pend_ok && (!kPhaseLock || it_odd)) nw = first_win(pend_o0) | 2u;   /* the next iteration is even */
       wait_lgkm0();
       issue();
     }
@@ -1936,6 +1961,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     }
     }
     wpos += (int32_t) kWBlock;
+    it_odd ^= 1u;
     dg.iteration_end();
     if (!__ballot(dhas || nw || pend_ok)) break;
   }

@@ -323,7 +323,7 @@ RHP_DHD constexpr bool idx_used(uint32_t i) { return i < kRows2 && state2(i) < S
  * 256-byte rows.
  */
 struct RowLayout {
-  uint32_t row[2 + kClasses];   /* kClassRow, kClassRowR, code_row(0..14) */
+  uint32_t row[3 + kClasses];   /* kClassRow, kClassRowR, kClassRow16, code_row(0..14) */
   uint32_t bytes;               /* the table's size, 16-byte multiple */
 };
 constexpr RowLayout make_row_layout()
@@ -332,7 +332,7 @@ constexpr RowLayout make_row_layout()
   uint32_t end = 0, n = 0;
   for (uint32_t i = 0; i < kRows2; i++)
     if (idx_used(i) && i * kStride + kCodes > end) end = i * kStride + kCodes;
-  for (uint32_t r = 0; r < 256u && n < 2u + kClasses; r++) {
+  for (uint32_t r = 0; r < 256u && n < 3u + kClasses; r++) {
     bool free = true;
     for (uint32_t i = 0; i < kRows2; i++)
       if (idx_used(i) && i * kStride < r * 256u + 256u && r * 256u < i * kStride + kCodes) free = false;
@@ -341,7 +341,7 @@ constexpr RowLayout make_row_layout()
       if (r * 256u + 256u > end) end = r * 256u + 256u;
     }
   }
-  l.bytes = n == 2u + kClasses ? (end + 15u) & ~15u : 0u;
+  l.bytes = n == 3u + kClasses ? (end + 15u) & ~15u : 0u;
   return l;
 }
 constexpr RowLayout kRowLayout = make_row_layout();
@@ -349,9 +349,10 @@ static_assert(kRowLayout.bytes != 0, "the lookup rows fit");
 enum : uint32_t {
   kClassRow = kRowLayout.row[0],
   kClassRowR = kRowLayout.row[1],
+  kClassRow16 = kRowLayout.row[2],   /* class(b) * 16: the b0 half of a code (the kernel's code form 2) */
   kTable2Bytes = kRowLayout.bytes
 };
-RHP_DHD constexpr uint32_t code_row(uint32_t k) { return kRowLayout.row[2 + k]; }   /* k < kClasses */
+RHP_DHD constexpr uint32_t code_row(uint32_t k) { return kRowLayout.row[3 + k]; }   /* k < kClasses */
 static_assert(kClassRowR < 256u && code_row(kClasses - 1u) < 256u, "row numbers are bytes");
 
 RHP_DHD constexpr bool is_done2(uint32_t i) { return state2(i) == S_DONE || state2(i) == S_DONE_E; }
@@ -379,6 +380,7 @@ constexpr Table2 make_table2()
   }
   for (uint32_t c = 0; c < 256; c++) t.b[kClassRow * 256u + c] = (uint8_t) byte_class(c);
   for (uint32_t c = 0; c < 256; c++) t.b[kClassRowR * 256u + c] = (uint8_t) code_row(byte_class(c));
+  for (uint32_t c = 0; c < 256; c++) t.b[kClassRow16 * 256u + c] = (uint8_t) (byte_class(c) * 16u);
   for (uint32_t k = 0; k < kClasses; k++)
     for (uint32_t c = 0; c < 256; c++) t.b[code_row(k) * 256u + c] = (uint8_t) (byte_class(c) * 16u + k);
   return t;

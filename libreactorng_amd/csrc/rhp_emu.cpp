@@ -252,6 +252,23 @@ extern "C" int rhp_test_chunk_window(const uint8_t *line, uint32_t nw, uint64_t 
   return one_chunk_window(W, nw, avail, res, doff, dlen) ? 1 : 0;
 }
 
+/* test hook: the pair table the kernel copies into LDS (rhp_dfa.h make_table2)
+ * and its geometry: meta = {bytes, row stride, kClassRowR, kClassRow, idx2(S_SLOW, 1), kClassRow16} */
+extern "C" uint32_t rhp_test_table2(uint8_t *out, uint32_t *meta)
+{
+  const Table2 &t = table();
+  if (out) memcpy(out, t.b, kTable2Bytes);
+  if (meta) {
+    meta[0] = kTable2Bytes;
+    meta[1] = kStride;
+    meta[2] = kClassRowR;
+    meta[3] = kClassRow;
+    meta[4] = idx2(S_SLOW, 1);
+    meta[5] = kClassRow16;
+  }
+  return kTable2Bytes;
+}
+
 /* test hook: one_chunk_t over `body` (size bytes, readable to size + 64) */
 extern "C" int64_t rhp_test_chunk_exact(const uint8_t *body, uint64_t at, uint64_t size, uint64_t *doff, uint64_t *dlen)
 {

@@ -143,6 +143,10 @@ static_assert(idx2(S_DONE, 0) == kPark, "parked lanes sit in DONE");
  * the kernel's window geometry) and the waves its staging leaves room for */
 constexpr uint32_t kHttpXParts = RHP_HTTP_XPARTS;   /* rhp_dfa.h: the emulator walks the same windows */
 constexpr int kHttpWaves = kHttpXParts == 0 ? 16 : kHttpXParts <= 2 ? 12 : 8;
+#ifndef RHP_CODE_FORM
+#define RHP_CODE_FORM 1
+#endif
+constexpr int kCodeForm = RHP_CODE_FORM;   /* how a pair's code is looked up (the walk's look_a / look_b) */
 /* the lowest pair index of a state that is not terminal (DONE, ERR, SLOW and
  * their event forms are the indices below it) */
 constexpr uint32_t kLiveIdx = idx2(S_SLOW, 1) + 1u;
@@ -1642,25 +1646,36 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     return true;
   };
 
-  /* Pair codes by two lookups (rhp_dfa.h code_row): A = the row of class(b1),
-   * B = class(b0) * 16 + class(b1) from that row.  The table sits at LDS
-   * address 0, so a v_perm result is the address itself. */
+  /* Pair codes by two lookups.  Form 1 (rhp_dfa.h code_row): A = the row of
+   * class(b1), B = class(b0) * 16 + class(b1) from that row: the code read's
+   * address is one v_perm, but lanes whose b0 share an LDS bank and whose b1
+   * differ in class read different rows there (a bank conflict: 3.25 LDS cycles
+   * per read on config 2 where 2 is conflict free, tools/lds_conflicts.py).
+   * Form 2 (RHP_CODE_FORM=2): A = class(b1), B = class(b0) * 16, each from one
+   * 256-byte row (conflict free for bytes < 0x80), code = A | B: one more
+   * v_or per pair.  The table sits at LDS address 0, so a v_perm result is the
+   * address itself. */
+  auto look_a = [&](uint32_t dw, int j) -> uint32_t {
+    return lds_u8(__builtin_amdgcn_perm(kCodeForm == 2 ? kClassRow : kClassRowR, dw, 0x0c0c0400u | (uint32_t) (2 * (j & 1) + 1)));
+  };
+  auto look_b = [&](uint32_t a, uint32_t dw, int j) -> uint32_t {
+    return lds_u8(__builtin_amdgcn_perm(kCodeForm == 2 ? kClassRow16 : a, dw, 0x0c0c0400u | (uint32_t) (2 * (j & 1))));
+  };
+  auto code_of = [&](uint32_t a, uint32_t b) -> uint32_t { return kCodeForm == 2 ? (a | b) : b; };
   auto codes_a = [&](const u32x4 &chunk, uint32_t (&r)[8]) {
 #pragma unroll
-    for (int j = 0; j < 8; j++)
-      r[j] = lds_u8(__builtin_amdgcn_perm(kClassRowR, chunk[j >> 1], 0x0c0c0400u | (uint32_t) (2 * (j & 1) + 1)));
+    for (int j = 0; j < 8; j++) r[j] = look_a(chunk[j >> 1], j);
   };
   auto codes_b = [&](const u32x4 &chunk, const uint32_t (&r)[8], uint32_t (&c)[8]) {
 #pragma unroll
-    for (int j = 0; j < 8; j++)
-      c[j] = lds_u8(__builtin_amdgcn_perm(r[j], chunk[j >> 1], 0x0c0c0400u | (uint32_t) (2 * (j & 1))));
+    for (int j = 0; j < 8; j++) c[j] = code_of(r[j], look_b(r[j], chunk[j >> 1], j));
   };
   /* The walk of the window in W: part 0's codes first, then per chained step
    * one independent lookup pair for the next part behind the step's read (its
-   * class-row read, and the code read of the step before, whose class row has
-   * landed by then).  LDS returns in order, so a step waits only for its own
-   * read while the lookups fly behind it (issued ahead of it, a batch of eight
-   * delayed every fourth step: config 2 +3 %). */
+   * A read, and the B read of the step before, whose A has landed by then).
+   * LDS returns in order, so a step waits only for its own read while the
+   * lookups fly behind it (issued ahead of it, a batch of eight delayed every
+   * fourth step: config 2 +3 %). */
   auto walk = [&]() {
     uint32_t c[8], r[8];
     codes_a(W[0], r);
@@ -1673,18 +1688,16 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       for (int j = 0; j < 8; j++) {
         st = lds_u8(row_addr(st, c[j]));
         __builtin_amdgcn_sched_barrier(0);   /* the chained read issues first */
-        if (nx)
-          r[j] = lds_u8(__builtin_amdgcn_perm(kClassRowR, W[q + 1][j >> 1], 0x0c0c0400u | (uint32_t) (2 * (j & 1) + 1)));
-        if (nx && j > 0)
-          cn[j - 1] = lds_u8(__builtin_amdgcn_perm(r[j - 1], W[q + 1][(j - 1) >> 1], 0x0c0c0400u | (uint32_t) (2 * ((j - 1) & 1))));
+        if (nx) r[j] = look_a(W[q + 1][j >> 1], j);
+        if (nx && j > 0) cn[j - 1] = look_b(r[j - 1], W[q + 1][(j - 1) >> 1], j - 1);
         __builtin_amdgcn_sched_barrier(0);
         ev_shift2(ev[q >> 1], st);
         __builtin_amdgcn_sched_barrier(0);
       }
       if (nx) {
-        cn[7] = lds_u8(__builtin_amdgcn_perm(r[7], W[q + 1][3], 0x0c0c0400u | 2u));
+        cn[7] = look_b(r[7], W[q + 1][3], 7);
 #pragma unroll
-        for (int j = 0; j < 8; j++) c[j] = cn[j];
+        for (int j = 0; j < 8; j++) c[j] = code_of(r[j], cn[j]);
       }
       /* phase-locked http form: once every lane of the wave is terminal (or
        * parked) the rest of the window changes nothing -- terminal states are

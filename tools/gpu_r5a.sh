@@ -18,8 +18,9 @@ PY
 }
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r5a/pytest_parity.log 2>&1 \
   && echo PARITY_OK && tail -2 gpurun_out/r5a/pytest_parity.log \
-  && ab base base "" && ab s260 s260 "" \
-  && for r in 1 2; do ab dx dx "" && ab dxs dxs "" && ab cx cx "post=compact,chunked=compact" && ab pl pl "post=compact,chunked=compact" || exit 1; done \
+  && ab base base "" && ab s260 s260 "" && ab dx dx "" && ab dxs dxs "" && ab cx cx "post=compact,chunked=compact" \
+  && ab pl pl "post=compact,chunked=compact" && ab cf2 cf2 "post=compact,chunked=compact" && ab cf2s cf2s "post=compact,chunked=compact" \
+  && ab dx dx "" && ab cf2s cf2s "post=compact,chunked=compact" && ab pl pl "post=compact,chunked=compact" \
   && cat gpurun_out/r5a/ab.txt \
   && RHP_LIB=$L/librhp_x_stamps.so STAMPS_CFG=2,3,5 timeout -k 10 240 python tools/stamps2.py > gpurun_out/r5a/stamps_committed.txt 2>&1 \
   && RHP_LIB=$L/librhp_x_stampsdx.so STAMPS_CFG=2,3,5 timeout -k 10 240 python tools/stamps2.py > gpurun_out/r5a/stamps_dx.txt 2>&1 \

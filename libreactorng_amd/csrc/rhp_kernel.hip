@@ -1710,14 +1710,24 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 
   /* LDS-DMA of every lane's next window (nw) into the staging buffer:
    * kParts loads of 1 KiB (see stage_off) */
-  auto issue = [&]() {
-    /* all shuffles first (one LDS round trip for the lot), then the loads; a
-     * lane without a next window fetches the range's first bytes instead (its
-     * staging slot is not read), so no load needs a branch */
-    const uint32_t src = (nw & 3u) ? (nw & ~3u) : 0u;
+  /* In two halves: issue_prep exchanges the window addresses (the shuffles,
+   * one LDS round trip for the lot), issue_go makes the loads once the caller
+   * has waited for its LDS reads -- the shuffles are issued before the reads
+   * the wait is for, so the issue costs no round trip of its own */
+  struct Issue {
     uint32_t a[kParts];
+    uint32_t src;
+  };
+  auto issue_prep = [&](Issue &is) {
+    /* a lane without a next window fetches the range's first bytes instead
+     * (its staging slot is not read), so no load needs a branch */
+    is.src = (nw & 3u) ? (nw & ~3u) : 0u;
 #pragma unroll
-    for (int i = 0; i < (int) kParts; i++) a[i] = (uint32_t) __shfl((int) src, (int) dma_window((uint32_t) i, lane));
+    for (int i = 0; i < (int) kParts; i++) is.a[i] = (uint32_t) __shfl((int) is.src, (int) dma_window((uint32_t) i, lane));
+  };
+  auto issue_go = [&](const Issue &is) {
+    const uint32_t src = is.src;
+    const uint32_t (&a)[kParts] = is.a;
     /* Cache policy per wave and window: when every window is one whole HBM
      * line (line-aligned requests), no line is read by two windows and the
      * loads go non-temporal (config 2 +19 %, config 5 +9 %); windows that
@@ -1740,6 +1750,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     for (uint32_t k = 0; k < kXParts; k++)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (__attribute__((address_space(3))) void *) (lds + xstage + 1024u * k),
                                                16, src + kBlock + 16u * k, 0, 0, 0);
+  };
+  auto issue = [&]() {
+    Issue is;
+    issue_prep(is);
+    issue_go(is);
   };
 
   /* Uneven ranges (config 3) order the hand-out from the first request on;
@@ -1872,18 +1887,23 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     if (nw_kind) cur_ptr = nw & ~3u;
     const bool walking = nw_kind != 0 && wact;   /* a live request's window landed */
     const bool pend_ready = pend_ok;   /* assigned before this block: its offsets are valid */
+    Issue is;
+    if constexpr (!LATE) {
+      /* [E] next window: continuation of wcur, else the first window of a ready
+       * pend (its addresses exchanged now, the loads made after [D]) */
+      nw = 0;
+      if (walking && (uint32_t) (wpos + (int32_t) kWBlock) < wlen) nw = (cur_ptr + kWBlock) | 1u;
+      else if (pend_ready) nw = first_win(p_o0) | 2u;
+      issue_prep(is);
+    }
     /* [D] */
     refill_pend();
     const bool any_walk = __builtin_amdgcn_ballot_w64(walking) != 0;
     const bool any_dec = __builtin_amdgcn_ballot_w64(dhas) != 0;
     dg.lanes(walking, pool_dry);
     if constexpr (!LATE) {
-      /* [E] next window: continuation of wcur, else the first window of a ready pend */
-      nw = 0;
-      if (walking && (uint32_t) (wpos + (int32_t) kWBlock) < wlen) nw = (cur_ptr + kWBlock) | 1u;
-      else if (pend_ready) nw = first_win(p_o0) | 2u;
-      wait_lgkm0();   /* [A]'s reads of the buffer are done */
-      issue();
+      wait_lgkm0();   /* [A]'s reads of the buffer and the shuffles are done */
+      issue_go(is);
       dg.section(1, true);
       /* [F] walk + decode of the previous window */
       decode_begin();
@@ -1944,7 +1964,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       nw = 0;
       if (walking && wact) nw = (cur_ptr + kWBlock) | 1u;
       else if (pend_ok && (!kPhaseLock || it_odd)) nw = first_win(pend_o0) | 2u;   /* the next iteration is even */
-      wait_lgkm0();
+      wait_lgkm0();   /* the decode's reads of the buffer are done */
       issue();
     }
     dg.section(LATE ? 4 : 3, true);

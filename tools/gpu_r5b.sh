@@ -4,6 +4,19 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT}" && mkdir -p gpurun_out/r5b && export TMPDIR=/tmp
 L=$PWD/libreactorng_amd
+ab() {   # name lib layouts-env
+  RHP_LIB=$L/librhp_x_$2.so RHP_BENCH_LAYOUTS=$3 timeout -k 10 300 python bench.py --no-cpu --no-e2e --steps 30 --warmup 5 --extra-steps 15 \
+    > gpurun_out/r5b/ab_$1.json 2>/dev/null || { echo "FAIL $1"; return 1; }
+  python3 - gpurun_out/r5b/ab_$1.json $1 >> gpurun_out/r5b/ab.txt <<'PY'
+import json, sys
+d = json.load(open(sys.argv[1])); e = d.get("extra_configs", {})
+k = lambda c: e.get(c, {}).get("roofline", {}).get("kernel_ms", 0) * 1e3
+print(f"{sys.argv[2]:8s} c2 {d['roofline']['kernel_ms']*1e3:6.1f} us wall {d['ms_per_step']*1e3:6.1f} us  c3 {k('zipf'):6.1f}  c5 {k('post'):6.1f}  "
+      f"chunked {k('chunked'):7.1f}  parity {sorted(set(v if isinstance(v, str) else v.get('result') for v in d.get('parity', {}).values()))}")
+PY
+}
+C="post=compact,chunked=compact"
+for r in 1 2; do ab pl pl $C && ab ip ip $C && ab ipc ipc $C || exit 1; done && cat gpurun_out/r5b/ab.txt
 for v in dx ladiag; do
   RHP_LIB=$L/librhp_x_$v.so RHP_BENCH_DIAG=1 timeout -k 10 300 python bench.py --config zipf --extra none --no-cpu --no-e2e --steps 30 --warmup 5 \
     > gpurun_out/r5b/zipf_$v.json 2>/dev/null || exit 1

@@ -87,11 +87,17 @@ __device__ __forceinline__ void mark_wide(const Params &p, uint32_t i)
 {
   if (p.hc) store_hc(p, i, RHP_HTTP_WIDE << 16, 0u);
 }
-/* a final record whose consumed is ret (+ body_len for a Content-Length body), or 0 */
+/* a final record whose consumed is ret (+ body_len for a Content-Length body,
+ * mod 2^64 as http.c:216), or 0; a body_len past 32 bits (a Content-Length
+ * whose ret + size wrapped, or a body beyond 4 GiB) keeps the wide record */
 __device__ __forceinline__ void put_http(const Params &p, uint32_t i, const rhp_http_t &o)
 {
-  if (p.hc) store_hc(p, i, ((uint32_t) o.result & 0xffu) | o.body_kind << 8, (uint32_t) o.body_len);
-  else p.http[i] = o;
+  if (p.hc && !(o.body_len >> 32)) {
+    store_hc(p, i, ((uint32_t) o.result & 0xffu) | o.body_kind << 8, (uint32_t) o.body_len);
+  } else {
+    p.http[i] = o;
+    mark_wide(p, i);
+  }
 }
 
 #ifndef RHP_WAVES_PER_SIMD
@@ -1610,7 +1616,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
                 x.body_kind = 1; x.body_len = size; x.consumed = (uint64_t) ret + size;
               }
             }
-            if constexpr (COMPACT) store_hc(p, dcur, ((uint32_t) x.result & 0xffu) | x.body_kind << 8, (uint32_t) x.body_len);
+            if constexpr (COMPACT) put_http(p, dcur, x);
             else store_http(p.http + dcur, x);
             framed = true;
           }

@@ -24,4 +24,4 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 1
   && cat gpurun_out/r5a/ab.txt \
   && RHP_LIB=$L/librhp_x_stamps.so STAMPS_CFG=2,3,5 timeout -k 10 240 python tools/stamps2.py > gpurun_out/r5a/stamps_committed.txt 2>&1 \
   && RHP_LIB=$L/librhp_x_stampsdx.so STAMPS_CFG=2,3,5 timeout -k 10 240 python tools/stamps2.py > gpurun_out/r5a/stamps_dx.txt 2>&1 \
-  && RHP_LIB=$L/librhp_x_stampspl.so STAMPS_CFG=5 timeout -k 10 240 python tools/stamps2.py > gpurun_out/r5a/stamps_pl.txt 2>&1 && echo STAMPS_OK
+  && RHP_LIB=$L/librhp_x_stampspl.so STAMPS_CFG=2,5 timeout -k 10 240 python tools/stamps2.py > gpurun_out/r5a/stamps_pl.txt 2>&1 && echo STAMPS_OK

@@ -16,7 +16,7 @@ print(f"{sys.argv[2]:8s} c2 {d['roofline']['kernel_ms']*1e3:6.1f} us wall {d['ms
 PY
 }
 C="post=compact,chunked=compact"
-for r in 1 2; do ab pl pl $C && ab ip ip $C && ab ipc ipc $C || exit 1; done && cat gpurun_out/r5b/ab.txt
+ab base base "" && ab cx cx $C && ab cf2 cf2 $C && ab cf2s cf2s $C && ab pl pl $C && cat gpurun_out/r5b/ab.txt || exit 1
 for v in dx ladiag; do
   RHP_LIB=$L/librhp_x_$v.so RHP_BENCH_DIAG=1 timeout -k 10 300 python bench.py --config zipf --extra none --no-cpu --no-e2e --steps 30 --warmup 5 \
     > gpurun_out/r5b/zipf_$v.json 2>/dev/null || exit 1

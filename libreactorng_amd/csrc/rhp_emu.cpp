@@ -197,6 +197,28 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
         r.num_headers = (uint16_t) d.nh;
         r.flags = 0;
         b->reqs[i] = r;
+        if (b->mode == RHP_MODE_HTTP && compact) {
+          /* as the kernel: with compact records a request that is not GET and
+           * has three or more framing candidates (names of 14 or 17 bytes), or
+           * one at header index >= 30, is framed by the exact path (its http_frame
+           * has no rhp_hdr_t records to read) */
+          uint32_t ncand = 0;
+          bool late = false;
+          for (uint32_t k = 0; k < d.nh && k < maxh; k++) {
+            const uint32_t nl = lens[(uint64_t) k * b->n] & 0xffffu;
+            if (nl == 14u || nl == 17u) {
+              ncand++;
+              late |= k >= 30u;
+            }
+          }
+          const bool get = len >= 4 && memcmp(b->bytes + off, "GET ", 4) == 0;
+          if (!get && (ncand >= 3 || late)) {
+            st_count.fast_ok--;
+            st_count.exact++;
+            emu_exact(b, i, off, len);
+            break;
+          }
+        }
         if (b->mode == RHP_MODE_HTTP) {
           rhp_http_t x;
           if (compact) {   /* http_frame reads rhp_hdr_t records: the lengths expanded */

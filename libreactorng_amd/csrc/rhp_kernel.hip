@@ -215,23 +215,23 @@ struct Diag {
 #ifdef RHP_STAMPS
   unsigned long long t0 = 0, t1 = 0, c0 = 0, c1 = 0, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rp[6] = {0, 0, 0, 0, 0, 0};
   unsigned long long rt_entry = 0, rt_loads = 0, rt_loop = 0, n_walk = 0, n_idle = 0, n_idle_live = 0, n_dry = 0;
-  __device__ static unsigned long long now()
+  __device__ __forceinline__ static unsigned long long now()
   {
     __builtin_amdgcn_sched_barrier(0);
     const unsigned long long t = __builtin_amdgcn_s_memtime();
     __builtin_amdgcn_sched_barrier(0);
     return t;
   }
-  __device__ unsigned long long *slots(uint32_t waves) const
+  __device__ __forceinline__ unsigned long long *slots(uint32_t waves) const
   {
     return g_stamps + ((blockIdx.x * waves + (threadIdx.x >> 6)) % 8192u) * kStampSlots;
   }
-  __device__ void entry() { rt_entry = __builtin_amdgcn_s_memrealtime(); }
-  __device__ void loads_landed() { rt_loads = __builtin_amdgcn_s_memrealtime(); }
-  __device__ void loop_start() { rt_loop = __builtin_amdgcn_s_memrealtime(); }
-  __device__ void mark() { t0 = now(); }
+  __device__ __forceinline__ void entry() { rt_entry = __builtin_amdgcn_s_memrealtime(); }
+  __device__ __forceinline__ void loads_landed() { rt_loads = __builtin_amdgcn_s_memrealtime(); }
+  __device__ __forceinline__ void loop_start() { rt_loop = __builtin_amdgcn_s_memrealtime(); }
+  __device__ __forceinline__ void mark() { t0 = now(); }
   /* the section that began at the last mark ends here: its cycles into acc[k] */
-  __device__ void section(uint32_t k, bool lgkm = false, bool vm = false)
+  __device__ __forceinline__ void section(uint32_t k, bool lgkm = false, bool vm = false)
   {
     if (vm) wait_vm0();
     if (lgkm) wait_lgkm0();
@@ -239,15 +239,15 @@ struct Diag {
     acc[k] += t1 - t0;
     t0 = t1;
   }
-  __device__ void lanes(bool walking, bool pool_dry)
+  __device__ __forceinline__ void lanes(bool walking, bool pool_dry)
   {
     n_walk += __popcll(__builtin_amdgcn_ballot_w64(walking));
     n_idle += __popcll(__builtin_amdgcn_ballot_w64(!walking));
     if (!pool_dry) n_idle_live += __popcll(__builtin_amdgcn_ballot_w64(!walking));
     else n_dry++;
   }
-  __device__ void iteration_end() { section(4); acc[5] += 1; }
-  __device__ void loop_end(uint32_t waves)
+  __device__ __forceinline__ void iteration_end() { section(4); acc[5] += 1; }
+  __device__ __forceinline__ void loop_end(uint32_t waves)
   {
     if ((threadIdx.x & 63u) != 0) return;
     unsigned long long *g = slots(waves);
@@ -256,18 +256,18 @@ struct Diag {
     g[10] = n_walk; g[11] = n_idle; g[12] = n_idle_live; g[13] = n_dry; g[19] = rt_loads;
     g[20] = acc[kSecDecodeStamp]; g[21] = acc[kSecFrameStamp];
   }
-  __device__ void replay_start(uint32_t waves)
+  __device__ __forceinline__ void replay_start(uint32_t waves)
   {
     if ((threadIdx.x & 63u) == 0) slots(waves)[14] = __builtin_amdgcn_s_memrealtime();
   }
-  __device__ void pass_begin() { c0 = now(); }
-  __device__ void pass_end(uint32_t k) { rp[k] += now() - c0; }   /* 0: pass 2, 1: pass 1 */
-  __device__ void framed(bool done) { rp[3] += __popcll(__builtin_amdgcn_ballot_w64(done)); }
-  __device__ void slow_path() { rp[2] += __popcll(__builtin_amdgcn_ballot_w64(true)); }
+  __device__ __forceinline__ void pass_begin() { c0 = now(); }
+  __device__ __forceinline__ void pass_end(uint32_t k) { rp[k] += now() - c0; }   /* 0: pass 2, 1: pass 1 */
+  __device__ __forceinline__ void framed(bool done) { rp[3] += __popcll(__builtin_amdgcn_ballot_w64(done)); }
+  __device__ __forceinline__ void slow_path() { rp[2] += __popcll(__builtin_amdgcn_ballot_w64(true)); }
   /* pass 2's parts: 4 the lanes' validation / serial paths, 5 the wave's staged moves */
-  __device__ void part_begin() { c1 = now(); }
-  __device__ void part_end(uint32_t k) { rp[k] += now() - c1; }
-  __device__ void exit(uint32_t waves)
+  __device__ __forceinline__ void part_begin() { c1 = now(); }
+  __device__ __forceinline__ void part_end(uint32_t k) { rp[k] += now() - c1; }
+  __device__ __forceinline__ void exit(uint32_t waves)
   {
     if ((threadIdx.x & 63u) != 0) return;
     unsigned long long *g = slots(waves);

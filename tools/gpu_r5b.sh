@@ -1,6 +1,6 @@
 #!/bin/bash
-# round 5 session b: line-window diagnostic (time + FETCH of config 3), SQ counters per config on the
-# new decode, reactor round timeline
+# round 5 session b: stamps (inlined diagnostics) of the phase-locked kernel, config 5 record layouts
+# with the lock, line-window diagnostic (time + FETCH of config 3), SQ counters per config, reactor timeline
 set -o pipefail
 cd "${GRAFT_REPO_ROOT}" && mkdir -p gpurun_out/r5b && export TMPDIR=/tmp
 L=$PWD/libreactorng_amd
@@ -15,13 +15,13 @@ print(f"{sys.argv[2]:8s} c2 {d['roofline']['kernel_ms']*1e3:6.1f} us wall {d['ms
       f"chunked {k('chunked'):7.1f}  parity {sorted(set(v if isinstance(v, str) else v.get('result') for v in d.get('parity', {}).values()))}")
 PY
 }
-C="post=compact,chunked=compact"
-ab base base "" && ab cx cx $C && ab cf2 cf2 $C && ab cf2s cf2s $C && ab pl pl $C && cat gpurun_out/r5b/ab.txt || exit 1
-for v in dx ladiag; do
+RHP_LIB=$L/librhp_x_stampspl.so STAMPS_CFG=2,3,5 timeout -k 10 240 python tools/stamps2.py > gpurun_out/r5b/stamps_pl.txt 2>&1 && echo STAMPS_OK && head -14 gpurun_out/r5b/stamps_pl.txt \
+ && ab plh pl "" && ab plc pl "post=compact,chunked=compact" && ab plh pl "" && ab plc pl "post=compact,chunked=compact" && cat gpurun_out/r5b/ab.txt || exit 1
+for v in pl ladiag; do
   RHP_LIB=$L/librhp_x_$v.so RHP_BENCH_DIAG=1 timeout -k 10 300 python bench.py --config zipf --extra none --no-cpu --no-e2e --steps 30 --warmup 5 \
     > gpurun_out/r5b/zipf_$v.json 2>/dev/null || exit 1
   RHP_LIB=$L/librhp_x_$v.so RHP_BENCH_DIAG=1 timeout -k 10 -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/r5b/pmc_${v}_zipf -o p \
     -- python3 bench.py --config zipf --extra none --steps 6 --warmup 2 --no-cpu --no-e2e > gpurun_out/r5b/pmc_${v}_zipf.log 2>&1 || exit 1
 done && echo LADIAG_OK \
- && for c in get256 zipf post chunked; do TAG=r5b/sq_$c CONFIG=$c RHP_LIB=$L/librhp_x_dx.so bash tools/pmc_sq.sh > gpurun_out/r5b/sq_$c.txt 2>&1 || exit 1; done && echo SQ_OK \
+ && for c in get256 zipf post chunked; do TAG=r5b/sq_$c CONFIG=$c RHP_LIB=$L/librhp_x_pl.so bash tools/pmc_sq.sh > gpurun_out/r5b/sq_$c.txt 2>&1 || exit 1; done && echo SQ_OK \
  && timeout -k 10 600 bash tools/reactor_timeline.sh > gpurun_out/r5b/reactor_timeline.txt 2>&1 && echo TIMELINE_OK

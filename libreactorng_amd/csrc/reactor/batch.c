@@ -70,7 +70,7 @@ typedef struct slot
    * round's H2D, parse, fix-up and D2H, and host clocks of its submit's end and
    * of the completion thread's wake-up */
   hipEvent_t   tev[5];
-  uint64_t     t_enqueued, t_wake;
+  uint64_t     t_enqueued, t_wake, t_h2d_call, t_launch_calls;
 } slot_t;
 
 typedef struct batch_state
@@ -130,10 +130,11 @@ static void batch_key_init(void)
 static uint64_t st_rounds, st_requests, st_ns;
 static int      st_on;
 /* RHP_REACTOR_STATS=2: sums over the rounds, ns (device phases from the events) */
-enum { PH_SUBMIT, PH_H2D, PH_PARSE, PH_FIXUP, PH_D2H, PH_DEVICE, PH_WAKE, PH_LOOP, PH_COUNT };
+enum { PH_SUBMIT, PH_H2D_CALL, PH_LAUNCH_CALLS, PH_H2D, PH_PARSE, PH_FIXUP, PH_D2H, PH_DEVICE, PH_WAKE, PH_LOOP, PH_COUNT };
 static uint64_t st_phase[PH_COUNT], st_tl_rounds;
 static const char *const st_phase_name[PH_COUNT] = {
-  "submit (host: H2D, kernels, D2H enqueued)", "H2D", "rhp_parse_batch", "rhp_fixup_sessions", "D2H records",
+  "submit (host: H2D, kernels, D2H enqueued)", "  of it the H2D call", "  of it the two launches",
+  "H2D", "rhp_parse_batch", "rhp_fixup_sessions", "D2H records",
   "device span (H2D start -> D2H end)", "submit -> completion thread awake", "completion thread -> loop takes the result"};
 
 static void host_parse(batch_state_t *b, int k);
@@ -468,9 +469,24 @@ void reactor_batch_submit(int k, uint32_t n, size_t bytes, uint32_t n_sessions)
         HIP(hipEventCreate(&s->tev[e]));
     HIP(hipEventRecord(s->tev[0], B->stream));
   }
+  const uint64_t t_h2d0 = tl ? now_ns() : 0;
   HIP(hipMemcpyAsync(s->d_buf, s->h_buf, s->in_size, hipMemcpyHostToDevice, B->stream));   /* bytes, offsets, sessions */
+  const uint64_t t_h2d1 = tl ? now_ns() : 0;
+  s->t_h2d_call = t_h2d1 - t_h2d0;
   if (tl)
+  {
     HIP(hipEventRecord(s->tev[1], B->stream));
+    static int once;
+    if (!once++)
+    {
+      hipPointerAttribute_t pa;
+      memset(&pa, 0, sizeof pa);
+      const hipError_t e = hipPointerGetAttributes(&pa, s->h_buf);
+      fprintf(stderr, "reactor round timeline: slot buffer %p: hipPointerGetAttributes %d, type %d (host pinned = %d)\n",
+              (void *) s->h_buf, (int) e, (int) pa.type, (int) hipMemoryTypeHost);
+    }
+  }
+  const uint64_t t_l0 = tl ? now_ns() : 0;
   /* the pieces speculatively, then every session walked in order from its
    * true request boundaries (include/rhp.h rhp_fixup_sessions): all of a
    * round's pipelined requests, bodies included, in this one round */
@@ -490,7 +506,10 @@ void reactor_batch_submit(int k, uint32_t n, size_t bytes, uint32_t n_sessions)
   if (rc != 0)
     die("rhp_fixup_sessions", rc);
   if (tl)
+  {
     HIP(hipEventRecord(s->tev[3], B->stream));
+    s->t_launch_calls = now_ns() - t_l0;
+  }
   /* the records: one asynchronous copy of the layout's output part (the
    * bytes, de-framed in place where a body is chunked, http.c:155, come back
    * only for a round that has such a body: reactor_batch_result) */
@@ -548,7 +567,8 @@ void reactor_batch_result(int k, reactor_batch_result_t *out)
         (void) hipEventElapsedTime(&ms[e], s->tev[e - 1], s->tev[e]);
       float span = 0;
       (void) hipEventElapsedTime(&span, s->tev[0], s->tev[4]);
-      const uint64_t add[PH_COUNT] = {s->t_enqueued - s->t_submit, (uint64_t) (ms[1] * 1e6f), (uint64_t) (ms[2] * 1e6f),
+      const uint64_t add[PH_COUNT] = {s->t_enqueued - s->t_submit, s->t_h2d_call, s->t_launch_calls,
+                                      (uint64_t) (ms[1] * 1e6f), (uint64_t) (ms[2] * 1e6f),
                                       (uint64_t) (ms[3] * 1e6f), (uint64_t) (ms[4] * 1e6f), (uint64_t) (span * 1e6f),
                                       s->t_wake - s->t_submit, t_result - s->t_wake};
       for (int k2 = 0; k2 < PH_COUNT; k2++)

@@ -105,8 +105,8 @@ __device__ __forceinline__ void put_http(const Params &p, uint32_t i, const rhp_
 #endif
 
 enum : uint32_t {
-  kSecDecodeStamp = 6,                           /* Diag section slots of the late form's decode / framing */
-  kSecFrameStamp = 7,
+  kSecDecodeStamp = 6,                           /* Diag section slots of the late form's decode / framing; */
+  kSecFrameStamp = 7,                            /* the early form's window reads + [C] / shuffles + [D] */
   kBlock = 128,                                  /* window bytes per lane per loop iteration (early form) */
   kParts = kBlock / 16,                          /* 16-byte parts per window */
   kEvWords = kBlock / 32,                        /* 32-bit event words per window */
@@ -1864,6 +1864,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     case 2: __builtin_amdgcn_s_setprio(2); break;
     default: __builtin_amdgcn_s_setprio(3);
     }
+#elif RHP_PRIO_MODE == 3
+    /* the gap between the window's landing and the next window's issue at the
+     * top priority; the rest of the iteration rotates among 0-2 (below) */
+    __builtin_amdgcn_s_setprio(3);
 #endif
     dg.mark();
     /* [A] */
@@ -1893,6 +1897,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     if (nw_kind) cur_ptr = nw & ~3u;
     const bool walking = nw_kind != 0 && wact;   /* a live request's window landed */
     const bool pend_ready = pend_ok;   /* assigned before this block: its offsets are valid */
+    if constexpr (!LATE) dg.section(kSecDecodeStamp, true);   /* early form, stamps: [A]'s window reads + [C] */
     Issue is;
     if constexpr (!LATE) {
       /* [E] next window: continuation of wcur, else the first window of a ready
@@ -1901,6 +1906,22 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (walking && (uint32_t) (wpos + (int32_t) kWBlock) < wlen) nw = (cur_ptr + kWBlock) | 1u;
       else if (pend_ready) nw = first_win(p_o0) | 2u;
       issue_prep(is);
+#ifndef RHP_REFILL_FIRST
+      /* the loads first, [D]'s refill (an LDS atomic round trip and the pending
+       * offsets' loads) after them: from the window's landing to the next
+       * window's issue a wave has nothing of its own in flight */
+      dg.section(kSecFrameStamp, true);   /* stamps: the shuffles */
+      wait_lgkm0();   /* [A]'s reads of the buffer and the shuffles are done */
+      issue_go(is);
+#endif
+#if RHP_PRIO_MODE == 3
+      prio_it = prio_it == 2u ? 0u : prio_it + 1u;
+      switch (prio_it) {
+      case 0: __builtin_amdgcn_s_setprio(0); break;
+      case 1: __builtin_amdgcn_s_setprio(1); break;
+      default: __builtin_amdgcn_s_setprio(2);
+      }
+#endif
     }
     /* [D] */
     refill_pend();
@@ -1908,8 +1929,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     const bool any_dec = __builtin_amdgcn_ballot_w64(dhas) != 0;
     dg.lanes(walking, pool_dry);
     if constexpr (!LATE) {
+#ifdef RHP_REFILL_FIRST
+      dg.section(kSecFrameStamp, true);   /* stamps: the shuffles and [D]'s refill */
       wait_lgkm0();   /* [A]'s reads of the buffer and the shuffles are done */
       issue_go(is);
+#endif
       dg.section(1, true);
       /* [F] walk + decode of the previous window */
       decode_begin();

@@ -48,9 +48,12 @@ for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, rhp.LA
           f"({it / used.sum():.1f} per wave), cycles per iteration per wave:")
     for k in range(5):
         print(f"   {names[k]:26s} {tot[k] / it:8.0f}  ({100 * tot[k] / tot.sum():.1f} %)")
-    if st[used, 20].sum() > 0:
+    if st[used, 20].sum() > 0 and mode == 1:
         print(f"     (late form: section 2 = decode_window {st[used, 20].sum() / it:.0f} + frame_window "
               f"{st[used, 21].sum() / it:.0f} + decode_end/finalize)")
+    elif st[used, 20].sum() > 0:
+        print(f"     (early form, before section C-E: window reads + switch {st[used, 20].sum() / it:.0f}, "
+              f"shuffles + refill {st[used, 21].sum() / it:.0f}; C-E is then the loads' issue)")
     loop = st[used, :5].sum(axis=1)
     print(f"   per wave: {loop.mean():.0f} cycles in the loop (min {loop.min():.0f}, max {loop.max():.0f})")
     rt = np.concatenate([st[used, 6:10], st[used, 14:15]], axis=1) * 10.0 / 1000.0   # us

@@ -840,6 +840,19 @@ void reactor_batch_prepare(void)
    * request through the whole protocol, waited for here. */
   static const char warm[] = "GET / HTTP/1.1\r\nHost: warm-up\r\n\r\n";
   const size_t n = sizeof warm - 1;
+  /* The first copy of a size the runtime hands to the DMA engine costs ~1.4 ms
+   * (tools/h2d_probe.c: 1427 us for the first 128-KiB copy of a process, 2 us
+   * after; a round of one request copies too little to reach that path), so
+   * the slots' whole capacity goes over and back once here */
+  for (int k = 0; k < REACTOR_BATCH_SLOTS; k++)
+  {
+    slot_t *s = &B->slot[k];
+    (void) reactor_batch_reserve(k, n, 1, 1);
+    memset(s->h_buf, 0, s->cap);
+    HIP(hipMemcpyAsync(s->d_buf, s->h_buf, s->cap, hipMemcpyHostToDevice, B->stream));
+    HIP(hipMemcpyAsync(s->h_buf, s->d_buf, s->cap, hipMemcpyDeviceToHost, B->stream));
+  }
+  HIP(hipStreamSynchronize(B->stream));
   for (int k = REACTOR_BATCH_SLOTS - 1; k >= 0; k--)
   {
     uint8_t *h = reactor_batch_reserve(k, n, 1, 1);

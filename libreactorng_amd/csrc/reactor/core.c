@@ -29,6 +29,7 @@
 #include <sys/timerfd.h>
 
 #include "reactor.h"
+#include "reactor_batch.h"
 #include "rhp.h"
 
 /* ---------------------------------------------------------------- data */
@@ -206,6 +207,11 @@ void reactor_destruct(void)
 {
   if (--core.ref)
     return;
+  /* the thread's batch parser state (streams, events, pinned and device slots,
+   * its completion thread) released here, on the owning thread;
+   * kept while the reactor lives, so servers opened one after another reuse
+   * its slots at the capacity they grew to */
+  reactor_batch_release();
   for (size_t i = 0; i < core.next_n; i++)
     free(core.next[i]);
   free(core.next);

@@ -212,7 +212,6 @@ static void rounds_release(void)
   free(R.waiting);
   R.waiting = NULL;
   R.n_waiting = R.cap_waiting = 0;
-  reactor_batch_release();   /* the parser's per-thread state, on this thread */
 }
 
 

@@ -51,6 +51,45 @@ static void run(const char *name, void *h, void *d, size_t n, hipStream_t s)
   HIP(hipEventDestroy(b));
 }
 
+/* the reactor's sequence: fresh pinned + device buffers, a tiny warm-up copy,
+ * then the host fills the input and copies it (first real copy of the buffer) */
+static void fresh(size_t n, hipStream_t s, int reuse)
+{
+  static void *h, *d;
+  double call = 0, dev = 0;
+  const int reps = 8;
+  char *src = malloc(n);
+  memset(src, 'x', n);
+  for (int r = 0; r < reps; r++) {
+    if (!reuse || !h) {
+      if (h) { HIP(hipHostFree(h)); HIP(hipFree(d)); }
+      HIP(hipHostMalloc(&h, 4u << 20, hipHostMallocDefault));
+      HIP(hipMalloc(&d, 4u << 20));
+      HIP(hipMemcpyAsync(d, h, 64, hipMemcpyHostToDevice, s));
+      HIP(hipStreamSynchronize(s));
+    }
+    memcpy(h, src, n);
+    hipEvent_t a, b;
+    HIP(hipEventCreate(&a));
+    HIP(hipEventCreate(&b));
+    const double t0 = now_us();
+    HIP(hipEventRecord(a, s));
+    HIP(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s));
+    const double t1 = now_us();
+    HIP(hipEventRecord(b, s));
+    HIP(hipStreamSynchronize(s));
+    float ms = 0;
+    HIP(hipEventElapsedTime(&ms, a, b));
+    call += t1 - t0;
+    dev += ms * 1e3;
+    HIP(hipEventDestroy(a));
+    HIP(hipEventDestroy(b));
+  }
+  printf("%-28s %8zu KiB: call %8.1f us, copy (events) %8.1f us\n", reuse ? "reactor sequence, reused" : "reactor sequence, fresh",
+         n >> 10, call / reps, dev / reps);
+  free(src);
+}
+
 int main(void)
 {
   hipStream_t s;
@@ -63,6 +102,10 @@ int main(void)
   h2 = aligned_alloc(4096, cap);
   memset(h2, 0, cap);
   HIP(hipHostRegister(h2, cap, hipHostRegisterDefault));
+  for (size_t n = 128u << 10; n <= (2u << 20); n *= 4) {
+    fresh(n, s, 0);
+    fresh(n, s, 1);
+  }
   for (size_t n = 64u << 10; n <= (8u << 20); n *= 2) {
     run("hipHostMalloc default", h0, d, n, s);
     run("hipHostMalloc non-coherent", h1, d, n, s);

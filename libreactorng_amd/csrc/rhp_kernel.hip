@@ -2225,16 +2225,40 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   dg.exit(WAVES);
 }
 
-/* rhp_fixup_sessions: one thread per session (rhp_scalar.h fixup_session_t) */
+/* rhp_fixup_sessions: one wave per session.  The wave first takes the
+ * session's leading pieces whose speculative record is the whole piece -- a
+ * request that ended exactly at the piece's end with no chunked body to
+ * de-frame, the common case of pipelined input -- 64 pieces per step: the
+ * sequential walk of the reference's loop would take each of them as it is, in
+ * its own slot (rhp_scalar.h fixup_session_t), so only req_start is written.
+ * From the first other piece on, lane 0 walks the rest as that loop does. */
 __global__ __launch_bounds__(256) void rhp_fixup_kernel(Params p, const rhp_session_t *sessions, uint32_t n_sessions,
                                                        rhp_session_result_t *results, uint64_t *req_start)
 {
   const FixupIO io{p.bytes_rw, p.offsets, p.reqs, p.hdrs, p.http, p.hs_req, p.hs_hdr, p.max_headers};
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_sessions; k += gridDim.x * blockDim.x) {
-    const rhp_session_t ss = sessions[k];
-    fixup_session_t(io, ss.piece_lo, ss.piece_hi, req_start, &results[k],
-                    [&](uint64_t at) { return LineBytes{p.bytes_rw + at, ~0ull, {0, 0, 0, 0}}; }, DevDechunk{});
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t k = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (k >= n_sessions) return;   /* wave-uniform */
+  const rhp_session_t ss = sessions[k];
+  uint32_t from = ss.piece_lo;
+  while (from < ss.piece_hi) {
+    const uint32_t j = from + lane;
+    bool whole = false;
+    uint64_t a = 0;
+    if (j < ss.piece_hi) {
+      const rhp_http_t x = p.http[j];
+      a = p.offsets[j];
+      whole = x.result == 1 && x.body_kind != RHP_BODY_CHUNKED_PENDING && x.consumed == p.offsets[j + 1] - a;
+    }
+    const uint64_t other = __builtin_amdgcn_ballot_w64(!whole && j < ss.piece_hi);
+    const uint32_t stop = other ? from + (uint32_t) __builtin_ctzll(other) : min(from + 64u, ss.piece_hi);
+    if (j < stop) req_start[j] = a;
+    from = stop;
+    if (other) break;
   }
+  if (lane == 0)
+    fixup_session_t(io, ss.piece_lo, ss.piece_hi, req_start, &results[k],
+                    [&](uint64_t at) { return LineBytes{p.bytes_rw + at, ~0ull, {0, 0, 0, 0}}; }, DevDechunk{}, from);
 }
 
 /* Exact-path-only kernel: one request per thread, grid-stride (RHP_IMPL_EXACT). */
@@ -2429,7 +2453,7 @@ int rhp_fixup_sessions(const rhp_batch_t *b, const rhp_session_t *sessions, uint
   prm.rec_req = prm.hs_req;
   prm.rec_hdr = prm.hs_hdr;
   prm.wt_records = false;
-  const uint32_t grid = (n_sessions + 255u) / 256u;
+  const uint32_t grid = (n_sessions + 3u) / 4u;   /* four sessions (waves) per workgroup */
   hipLaunchKernelGGL(rhp_fixup_kernel, dim3(grid), dim3(256), 0, s, prm, sessions, n_sessions, results, req_start);
   return (int) hipGetLastError();
 }

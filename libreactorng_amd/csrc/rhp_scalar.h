@@ -552,13 +552,17 @@ struct FixupIO {
   uint32_t max_headers;
 };
 
+/* p_from (>= p_lo): the walk resumes at piece p_from, every piece before it
+ * having been taken as it is (a whole-piece request whose records stay in
+ * their slot and whose start req_start already holds) */
 template <class MakeBytes, class DC = PlainDechunk>
 RHP_HD void fixup_session_t(const FixupIO &io, uint32_t p_lo, uint32_t p_hi, uint64_t *req_start,
-                            rhp_session_result_t *out, MakeBytes mk, const DC &dc = DC())
+                            rhp_session_result_t *out, MakeBytes mk, const DC &dc = DC(), uint32_t p_from = ~0u)
 {
+  if (p_from == ~0u) p_from = p_lo;
   const uint64_t b_lo = io.off[p_lo], b_hi = io.off[p_hi];
-  uint64_t pos = b_lo;
-  uint32_t slot = p_lo, j = p_lo, more = 0;
+  uint64_t pos = io.off[p_from];
+  uint32_t slot = p_from, j = p_from, more = 0;
   while (pos < b_hi) {
     if (slot == p_hi) { more = 1; break; }
     while (j < p_hi && io.off[j] < pos) j++;

@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <stdint.h>
 
 #define HIP(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %d at %d\n", (int) e_, __LINE__); exit(1); } } while (0)
 
@@ -90,6 +91,28 @@ static void fresh(size_t n, hipStream_t s, int reuse)
   free(src);
 }
 
+/* the CPU's own reads and writes of each kind of host memory (the reactor
+ * packs rounds into its slots and dispatches from them) */
+static void cpu_rw(const char *name, void *h, size_t n)
+{
+  char *src = malloc(n);
+  memset(src, 'y', n);
+  double tw = 0, tr = 0;
+  volatile uint64_t sink = 0;
+  for (int r = 0; r < 5; r++) {
+    const double t0 = now_us();
+    memcpy(h, src, n);
+    const double t1 = now_us();
+    uint64_t acc = 0;
+    for (size_t i = 0; i < n / 8; i++) acc += ((const uint64_t *) h)[i];
+    const double t2 = now_us();
+    sink += acc;
+    if (r) { tw += t1 - t0; tr += t2 - t1; }
+  }
+  printf("cpu %-28s %6zu KiB: write %6.2f GB/s, read %6.2f GB/s\n", name, n >> 10, n / (tw / 4) / 1e3, n / (tr / 4) / 1e3);
+  free(src);
+}
+
 int main(void)
 {
   hipStream_t s;
@@ -102,6 +125,14 @@ int main(void)
   h2 = aligned_alloc(4096, cap);
   memset(h2, 0, cap);
   HIP(hipHostRegister(h2, cap, hipHostRegisterDefault));
+  {
+    void *m = malloc(8u << 20);
+    cpu_rw("malloc", m, 8u << 20);
+    free(m);
+    cpu_rw("hipHostMalloc default", h0, 8u << 20);
+    cpu_rw("hipHostMalloc non-coherent", h1, 8u << 20);
+    cpu_rw("malloc + hipHostRegister", h2, 8u << 20);
+  }
   for (size_t n = 128u << 10; n <= (2u << 20); n *= 4) {
     fresh(n, s, 0);
     fresh(n, s, 1);

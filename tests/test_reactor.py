@@ -115,8 +115,12 @@ def test_burst_rounds_gpu_vs_host():
     # round completion by our own waiter thread blocked on the round's event
     # (RHP_REACTOR_COMPLETE=event, the default) rather than the HIP runtime's
     # host-function thread: 2.17 M req/s against the host parser's 2.19 M
-    # (profiles/r03/reactor/); the parse is ~10 % of a burst's time
-    assert gpu >= 0.8 * host, (gpu, host)
+    # (profiles/r03/reactor/); the parse is ~10 % of a burst's time.  Round 5
+    # (registered slots, the wave-per-session fixup at 6 us instead of 187):
+    # 2.07 M against 2.05 M, 16K-request rounds 2.80 M against 2.77 M and 65K
+    # 3.33 M against 3.12 M (profiles/r05/reactor/) -- the guard leaves 5 % for
+    # a shared box's noise
+    assert gpu >= 0.95 * host, (gpu, host)
 
 
 @pytest.mark.gpu

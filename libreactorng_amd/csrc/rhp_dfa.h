@@ -71,7 +71,7 @@ namespace rhp {
 enum State : uint32_t {
   /* plain rows (no event on entry) */
   S_DONE = 0, S_ERR, S_SLOW,                   /* terminals */
-  S_SKIP3, S_SKIP2, S_SKIP1,                   /* leading bytes of an unaligned window */
+  S_PRE,                                       /* the window's bytes before the request's first */
   S_METHOD0, S_METHOD, S_PATH0, S_PATH,
   S_V1, S_V2, S_V3, S_V4, S_V5, S_V6, S_V7, S_V8_0, S_V8_1, S_CRLF_RL,
   S_LINE0, S_NAME, S_VAL0, S_VALUE, S_VWS, S_VCR, S_END_CR,
@@ -111,6 +111,8 @@ constexpr bool c_tchar(uint32_t c)
 }
 constexpr bool c_ctl(uint32_t c) { return c < 0x20u || c == 0x7fu; }   /* CTL or DEL */
 constexpr bool c_ows(uint32_t c) { return c == ' ' || c == '\t'; }
+/* the byte class of 0x00: CTL or DEL other than HT, LF and CR (C_CTLX below) */
+RHP_DHD constexpr bool byte_class_ctlx(uint32_t c) { return (c < 0x20u && c != '\t' && c != '\n' && c != '\r') || c == 0x7fu; }
 
 /* one transition: the next state on byte c in state s (picohttpparser.c line refs) */
 constexpr uint32_t step(uint32_t s, uint32_t c)
@@ -119,9 +121,11 @@ constexpr uint32_t step(uint32_t s, uint32_t c)
   case S_DONE: case S_DONE_E: return S_DONE;
   case S_ERR: case S_ERR_E: return S_ERR;
   case S_SLOW: return S_SLOW;
-  case S_SKIP3: return S_SKIP2;
-  case S_SKIP2: return S_SKIP1;
-  case S_SKIP1: return S_METHOD0;
+  case S_PRE:       /* a window starts at or before the request: the kernel zeroes the bytes
+                       before its first one (a CTL, which then starts no request: the
+                       kernel sends a request whose own first byte is such a CTL to the
+                       exact path instead of walking it) */
+    return byte_class_ctlx(c) ? S_PRE : step(S_METHOD0, c);
   case S_METHOD0:   /* optional leading empty line (:345-352) -> exact path; ADVANCE_TOKEN (:71-94) */
     if (c == '\r' || c == '\n' || c == ' ') return S_SLOW;
     return c_ctl(c) ? S_ERR_E : S_METHOD;
@@ -247,6 +251,14 @@ constexpr uint32_t class_rep(uint32_t k)   /* a byte of class k */
   constexpr uint8_t rep[kClasses] = {0x00, '\t', '\n', '\r', ' ', ':', 'H', 'T', 'P', '/', '.', '0', '1', '!', '"'};
   return rep[k];
 }
+
+constexpr bool ctlx_exact()
+{
+  for (uint32_t c = 0; c < 256; c++)
+    if (byte_class_ctlx(c) != (byte_class(c) == C_CTLX)) return false;
+  return byte_class(0) == C_CTLX;
+}
+static_assert(ctlx_exact(), "byte_class_ctlx is the class of the zeroed bytes");
 
 /* every byte behaves like its class representative in every state */
 constexpr bool classes_exact()

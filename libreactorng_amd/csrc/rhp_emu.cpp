@@ -1,8 +1,12 @@
 /*
  * rhp_emu.cpp -- CPU emulation of rhp_dfa_kernel, for tests only.
  *
- * Runs the same pair transition table (rhp_dfa.h Table2), the same 4-byte window alignment
- * (SKIP states), the same 64-byte blocks with one event-mask decode per block
+ * Runs the same pair transition table (rhp_dfa.h Table2), windows starting in the
+ * same S_PRE state with the bytes before the request zeroed (a request whose
+ * first byte is of their class goes to the exact path, as in the kernel; the
+ * same window geometry: phr mode's first windows start at the 128-byte line
+ * holding the request, http mode's at its dword), the same blocks with one
+ * event-mask decode per block
  * (rhp_dfa.h dec_event) and the same finalize decisions as the kernel, one
  * request at a time on the host.  Lets the DFA design be checked against
  * the oracle on millions of requests without a GPU; the GPU tests then check
@@ -112,11 +116,16 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
 
   for (uint32_t i = 0; i < b->n; i++) {
     const uint64_t off = b->offsets[i], len = b->offsets[i + 1] - off;
-    const uint32_t mis = (uint32_t) off & 3u;
+    /* the kernel's first window: from the 128-byte line (phr mode) or the dword
+     * (http mode) holding the request's first byte, offsets from the batch's
+     * bytes.  The geometry decides, in rare cases, whether the DFA path or the
+     * exact path answers (a max_headers overflow whose colon lies in the window
+     * that also holds a SLOW, or lies past len): the flags follow it, the
+     * answers do not */
+    const uint32_t mis = (uint32_t) off & (b->mode == RHP_MODE_PHR ? 127u : 3u);
     const uint8_t *win = b->bytes + (off - mis);
     int32_t pos = -(int32_t) mis;
-    uint32_t s0 = mis == 0 ? S_METHOD0 : mis == 1 ? S_SKIP1 : mis == 2 ? S_SKIP2 : S_SKIP3;
-    uint32_t st = idx2(s0, 0);
+    uint32_t st = idx2(byte_class_ctlx(b->bytes[off]) ? S_SLOW : S_PRE, 0);
     Dec d;
     dec_reset(d);
     const bool compact = b->layout == RHP_LAYOUT_COMPACT;
@@ -135,7 +144,8 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
       for (int w = 0; w < words; w++) {
         uint32_t ev = 0;
         for (int k = 0; k < 32; k += 2) {   /* one table read per byte pair */
-          st = T.b[st * kStride + cls[win[32 * w + k]] * 16u + cls[win[32 * w + k + 1]]];
+          const int32_t at = block_pos + 32 * w + k;   /* the bytes before the request read as 0 */
+          st = T.b[st * kStride + (at < 0 ? 0u : cls[win[32 * w + k]]) * 16u + (at + 1 < 0 ? 0u : cls[win[32 * w + k + 1]])];
           ev |= (st & 3u) << k;
         }
         evw[w] = ev;

@@ -157,7 +157,7 @@ constexpr int kCodeForm = RHP_CODE_FORM;   /* how a pair's code is looked up (th
  * their event forms are the indices below it) */
 constexpr uint32_t kLiveIdx = idx2(S_SLOW, 1) + 1u;
 static_assert(idx2(S_DONE, 0) < kLiveIdx && idx2(S_ERR, 1) < kLiveIdx && idx2(S_DONE_E, 3) < kLiveIdx &&
-              idx2(S_ERR_E, 3) < kLiveIdx && idx2(S_SKIP3, 0) >= kLiveIdx && idx2(S_SP1_E, 2) >= kLiveIdx,
+              idx2(S_ERR_E, 3) < kLiveIdx && idx2(S_PRE, 0) >= kLiveIdx && idx2(S_SP1_E, 2) >= kLiveIdx,
               "terminal indices lie below every live one");
 #ifndef RHP_PHASE_LOCK
 #define RHP_PHASE_LOCK 1
@@ -1083,7 +1083,18 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     }
   }
   const uint64_t o_lo = pool_dry ? 0 : p.offsets[wg_lo], o_hi = pool_dry ? 0 : p.offsets[wg_hi];
-  const uint64_t base = o_lo & ~(uint64_t) 3;
+  /* Window starts.  phr mode fetches a request's first window from the
+   * 128-byte line holding its first byte (kLead = 127: up to 127 bytes before
+   * the request are walked in S_PRE, zeroed), so every window is a whole HBM
+   * line (a 128-byte aligned buffer: lines are counted from p.bytes, so the
+   * geometry, and with it the rare choice between the DFA and the exact path
+   * the emulator mirrors, does not depend on the buffer's address) and no line
+   * is fetched by two windows of one request.  http mode fetches from the dword
+   * holding it (kLead = 3): its requests are framed from the window (the GET
+   * check, frame_window) at positions the 4-byte alignment keeps in the first
+   * part. */
+  constexpr uint32_t kLead = HTTP ? 3u : 127u;
+  const uint64_t base = o_lo & ~(uint64_t) kLead;
   if (o_hi - base >= 0xFFFF0000ull) {
     /* The window offsets below are u32 from `base`: a workgroup whose range
      * spans ~4 GiB (a request of that size among its requests) parses its
@@ -1105,6 +1116,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   int32_t wpos = 0;                    /* request-relative position of the window's first byte */
   bool wact = false;                   /* wcur is live: its walk has not ended */
   uint32_t wcur = 0, wlen = 0, wget = 0, cur_ptr = 0;
+  uint32_t wlead = 0;                  /* bytes before wcur in its first window (wnew) */
   uint32_t woff = 0;                   /* wcur's first byte, offset from base (LATE http framing) */
   uint32_t ev[kWEv];                   /* events of the window being walked (32 bytes per word) */
   bool pend_ok = false;                /* pend: the lane's next request */
@@ -1117,17 +1129,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   /* the extension parts of the wave's windows (kXParts > 0): after the pool area */
   const uint32_t xstage = __builtin_amdgcn_readfirstlane(kLdsTable + WAVES * kStageWave + kPoolBytes +
                                                          (tid >> 6) * 1024u * kXParts);
-  /* the first window of the request starting at (low dword) o0: its 4-aligned
-   * start, offset from base.  RHP_DIAG_LINE_WINDOWS (diagnostic build, wrong
-   * records): the 128-byte line holding it, as line-aligned windows would
-   * fetch, for the traffic and time such windows cost */
-  auto first_win = [&](uint32_t o0) -> uint32_t {
-#ifdef RHP_DIAG_LINE_WINDOWS
-    const uint32_t l = (o0 & ~127u) - (uint32_t) base;
-    if ((o0 & ~127u) - (uint32_t) base <= (o0 & ~3u) - (uint32_t) base) return l;
-#endif
-    return (o0 & ~3u) - (uint32_t) base;
-  };
+  /* the first window of the request starting at (low dword) o0, offset from
+   * base, and the number of bytes before the request in it (see kLead) */
+  auto first_win = [&](uint32_t o0) -> uint32_t { return (o0 - (uint32_t) base) & ~kLead; };
+  auto lead_of = [&](uint32_t o0) -> uint32_t { return (o0 - (uint32_t) base) & kLead; };
   /* LDS address of part q of this lane's window */
   auto part_lds = [&](uint32_t q) -> uint32_t {
     return q < kParts ? stage + stage_off(lane, q) : xstage + 1024u * (q - kParts) + 16u * lane;
@@ -1208,8 +1213,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const uint32_t k = tid + j * WAVES * 64;
       wc[j] = 0;
       if (k < span_n) {
-        const uint64_t len = p.offsets[wg_lo + k + 1] - p.offsets[wg_lo + k];
-        wc[j] = (uint32_t) min((len + 3u + kBlock - 1u) / kBlock, (uint64_t) kOrderBuckets - 1u);
+        const uint64_t o = p.offsets[wg_lo + k], len = p.offsets[wg_lo + k + 1] - o;
+        wc[j] = (uint32_t) min((len + lead_of((uint32_t) o) + kBlock - 1u) / kBlock, (uint64_t) kOrderBuckets - 1u);
         atomicAdd(&bucket[wc[j]], 1u);
       }
     }
@@ -1714,6 +1719,21 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     }
   };
 
+  /* The bytes of a first window before its request (wlead of them) zeroed in
+   * the registers: S_PRE walks them (rhp_dfa.h) */
+  auto zero_lead = [&](bool wnew) {
+    if (!__builtin_amdgcn_ballot_w64(wnew && wlead != 0)) return;
+    const uint32_t l8 = wnew ? 8u * wlead : 0u;
+#pragma unroll
+    for (uint32_t q = 0; q < kLead / 16u + 1u && q < kWParts; q++)
+#pragma unroll
+      for (uint32_t d = 0; d < 4u; d++) {
+        const uint32_t p8 = 128u * q + 32u * d;   /* the dword's first bit */
+        const uint32_t sh = l8 > p8 ? min(l8 - p8, 32u) : 0u;
+        W[q][d] &= (uint32_t) (~0ull << sh);
+      }
+  };
+
   /* LDS-DMA of every lane's next window (nw) into the staging buffer:
    * kParts loads of 1 KiB (see stage_off) */
   /* In two halves: issue_prep exchanges the window addresses (the shuffles,
@@ -1884,15 +1904,24 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       wlen = p_o1 - p_o0;
       if constexpr (LATE) woff = p_o0 - (uint32_t) base;
       pend_ok = false;
-      const uint32_t mis = p_o0 & 3u;
-      st = idx2(mis == 0 ? S_METHOD0 : mis == 1 ? S_SKIP1 : mis == 2 ? S_SKIP2 : S_SKIP3, 0);
-      wpos = -(int32_t) mis;
+      wlead = lead_of(p_o0);
+      wpos = -(int32_t) wlead;
       wact = true;
       wnew = true;
-      /* GET: the request's first four bytes are "GET " (the DFA path parses
-       * the method from byte 0), read from the window already in registers */
-      const uint32_t head = __builtin_amdgcn_alignbyte(W[0][1], W[0][0], mis);
-      wget = head == ('G' | 'E' << 8 | 'T' << 16 | (uint32_t) ' ' << 24) ? 0x40000000u : 0u;
+      uint32_t first;   /* the request's first byte */
+      if constexpr (HTTP) {
+        /* GET: the request's first four bytes are "GET " (the DFA path parses
+         * the method from byte 0), read from the window already in registers */
+        const uint32_t head = __builtin_amdgcn_alignbyte(W[0][1], W[0][0], wlead);
+        wget = head == ('G' | 'E' << 8 | 'T' << 16 | (uint32_t) ' ' << 24) ? 0x40000000u : 0u;
+        first = head & 0xffu;
+      } else {
+        /* from the staging buffer (before the next issue refills it) */
+        first = lds_u8(stage + stage_off(lane, wlead >> 4) + (wlead & 15u));
+      }
+      /* S_PRE walks the zeroed bytes before the request (rhp_dfa.h): a first
+       * byte of their class goes to the exact path */
+      st = idx2(byte_class_ctlx(first) ? S_SLOW : S_PRE, 0);
     }
     if (nw_kind) cur_ptr = nw & ~3u;
     const bool walking = nw_kind != 0 && wact;   /* a live request's window landed */
@@ -1943,6 +1972,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       dg.section(2, true, true);
       if (any_walk) {
         if (!walking) st = kPark;   /* idle lanes step in the parked terminal state */
+        zero_lead(wnew);
         walk();
       }
     } else {
@@ -1959,6 +1989,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       for (int w = 0; w < (int) kWEv; w++) ev[w] = 0;
       if (any_walk) {
         if (!walking) st = kPark;
+        zero_lead(wnew);
         walk();
       }
       dg.section(3, true);

@@ -1760,7 +1760,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
      * straddle lines share their edge lines with the neighbouring requests'
      * windows, which then hit in L2 (non-temporal: config 3 -5 %) */
     const bool aligned = !(nw & 3u) || ((uint32_t) (uintptr_t) (wbytes + src) & (kBlock - 1u)) == 0;
+#ifdef RHP_NO_NT
+    const bool nt = false && aligned;
+#else
     const bool nt = !__builtin_amdgcn_ballot_w64(!aligned);
+#endif
     /* one branch per issue, not one per load (the cache policy is an immediate) */
 #define RHP_ISSUE_LOADS(AUX)                                                                             \
     _Pragma("unroll") for (int i = 0; i < (int) kParts; i++) {                                           \
@@ -1814,7 +1818,12 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * share of the rest still fits beside them (config 3: 16 waves 422 us, 12
    * waves 398 us, 8 waves 474 us).  The other waves only join the barriers and
    * the replay. */
-  constexpr uint32_t kUnevenWaves = WAVES > 12 ? 12u : (uint32_t) WAVES;   /* 10: 472 us, 11: 450, 13: 408, 14: 413 */
+#ifndef RHP_UNEVEN_WAVES
+#define RHP_UNEVEN_WAVES 12
+#endif
+  constexpr uint32_t kUnevenWaves = WAVES > RHP_UNEVEN_WAVES ? RHP_UNEVEN_WAVES : (uint32_t) WAVES;   /* 10: 472 us, 11: 450, 13: 408, 14: 413 */
+  /* the order lives in the last three waves' staging (sort_range): they must not walk */
+  static_assert(kUnevenWaves + 3u <= (uint32_t) WAVES, "the idle waves' staging holds the hand-out order");
   bool idle_wave = false;
   if (uneven) {
     /* the whole range longest first, the first hand-out included: a long

@@ -1723,13 +1723,13 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * the registers: S_PRE walks them (rhp_dfa.h) */
   auto zero_lead = [&](bool wnew) {
     if (!__builtin_amdgcn_ballot_w64(wnew && wlead != 0)) return;
-    const uint32_t l8 = wnew ? 8u * wlead : 0u;
+    const int32_t l8 = wnew ? (int32_t) (8u * wlead) : 0;
 #pragma unroll
     for (uint32_t q = 0; q < kLead / 16u + 1u && q < kWParts; q++)
 #pragma unroll
       for (uint32_t d = 0; d < 4u; d++) {
-        const uint32_t p8 = 128u * q + 32u * d;   /* the dword's first bit */
-        const uint32_t sh = l8 > p8 ? min(l8 - p8, 32u) : 0u;
+        /* the dword's bytes before the request: a v_sub, a v_med3, a 64-bit shift, a v_and */
+        const int32_t sh = min(max(l8 - (int32_t) (128u * q + 32u * d), 0), 32);
         W[q][d] &= (uint32_t) (~0ull << sh);
       }
   };

@@ -37,7 +37,10 @@ step_pmc() {
   done
 }
 step_sq() {
-  TAG=sq_${TAG} CONFIG=get256 bash tools/pmc_sq.sh > gpurun_out/sq_${TAG}.txt 2>&1 && echo SQ_OK
+  for c in ${SQ_CONFIGS:-get256 zipf post chunked}; do
+    TAG=sq_${TAG}_$c CONFIG=$c bash tools/pmc_sq.sh > gpurun_out/sq_${TAG}_$c.txt 2>&1 || return 1
+    echo SQ_${c}_OK
+  done
 }
 step_writer() {
   timeout -k 10 120 python3 tools/bench_writer.py > gpurun_out/writer_${TAG}.json 2>&1 \

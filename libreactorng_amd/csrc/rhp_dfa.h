@@ -312,7 +312,7 @@ RHP_DHD constexpr uint32_t state2(uint32_t idx)
  * further (one v_mad_u32_u24 instead of the v_perm).
  */
 #ifndef RHP_ROW_STRIDE
-#define RHP_ROW_STRIDE 256
+#define RHP_ROW_STRIDE 260   /* round 5: after line windows 1-2 % faster on configs 2/3/5 (profiles/r05/ab/) */
 #endif
 enum : uint32_t {
   kStride = RHP_ROW_STRIDE,

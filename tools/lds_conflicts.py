@@ -17,7 +17,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import libreactorng_amd as rhp  # noqa: E402
 
-S_METHOD0, S_SKIP1, S_SKIP2, S_SKIP3 = 6, 5, 4, 3
+S_SLOW, S_PRE = 2, 3   # rhp_dfa.h State
 
 
 def table():
@@ -51,12 +51,17 @@ def main():
     steps = 0
     for w in range(waves):
         req = np.arange(64 * w, 64 * w + 64)
-        s4 = (off[req] & ~np.uint64(3)).astype(np.int64)
-        mis = (off[req] & np.uint64(3)).astype(np.int64)
-        st = np.array([4 * [S_METHOD0, S_SKIP1, S_SKIP2, S_SKIP3][m] for m in mis], dtype=np.int64)
+        # the kernel's first windows: the 128-B line holding the request (phr mode), its
+        # dword (http mode); the bytes before the request read as 0 and walk in S_PRE
+        lead_mask = np.uint64(3 if cfg == rhp.GEN_POST1K else 127)
+        s4 = (off[req] & ~lead_mask).astype(np.int64)
+        lead = (off[req] & lead_mask).astype(np.int64)
+        first = buf[off[req].astype(np.int64)]
+        ctlx = ((first < 0x20) & (first != 9) & (first != 10) & (first != 13)) | (first == 0x7f)
+        st = np.where(ctlx, 4 * S_SLOW, 4 * S_PRE).astype(np.int64)
         for p in range(128):   # two 128-B windows per lane
-            b0 = buf[s4 + 2 * p].astype(np.int64)
-            b1 = buf[s4 + 2 * p + 1].astype(np.int64)
+            b0 = np.where(2 * p < lead, 0, buf[s4 + 2 * p]).astype(np.int64)
+            b1 = np.where(2 * p + 1 < lead, 0, buf[s4 + 2 * p + 1]).astype(np.int64)
             a_r = crr * 256 + b1
             r = T[a_r].astype(np.int64)
             a_c = r * 256 + b0

@@ -88,6 +88,10 @@ def lib() -> ctypes.CDLL:
     if _rhp is None:
         if not os.path.exists(LIBRHP):
             raise RuntimeError(f"{LIBRHP} missing: run __graft_entry__.build() (hipcc gfx950)")
+        try:   # torch first: its HIP runtime is then the one librhp.so binds to (one runtime per process;
+            import torch  # noqa: F401  loading librhp.so first made torch's device buffers foreign to it: error 100)
+        except ImportError:
+            pass
         _rhp = ctypes.CDLL(LIBRHP)
         _rhp.rhp_parse_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p]
         _rhp.rhp_parse_batch.restype = ctypes.c_int

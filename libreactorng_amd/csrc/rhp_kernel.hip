@@ -2240,9 +2240,53 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       }
       dg.part_end(4);
     };
+    /* Rounds are claimed from an LDS counter, not dealt out by wave index: the
+     * waves a SIMD dispatched last run the replay's moves up to ~55 % slower
+     * (RHP_STAMPS, chunked: 500 vs 780 us for the same four rounds, the
+     * workgroup's end set by its slowest wave), so the faster waves take more
+     * rounds (round 5) */
+    uint32_t *round_next = wg_counter + 2;   /* 0 since the prologue */
+    auto claim = [&]() -> uint32_t {
+#ifdef RHP_STATIC_ROUNDS
+      static_cast<void>(round_next);
+      return 0u;
+#else
+      uint32_t r = 0;
+      if (lane == 0) r = atomicAdd(round_next, 1u);
+      return 64u * __builtin_amdgcn_readfirstlane(r);
+#endif
+    };
+#ifdef RHP_STATIC_ROUNDS
     uint32_t kb = tid & ~63u;
+    auto next_kb = [&](uint32_t k) { return k + WAVES * 64; };
+#else
+    uint32_t kb = claim();
+    auto next_kb = [&](uint32_t) { return claim(); };
+#endif
+#if RHP_REPLAY_PRIO == 1
+    /* the waves a SIMD dispatched last at the higher priorities */
+    switch ((tid >> 8) & 3u) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3);
+    }
+#endif
+    uint32_t rp = (tid >> 8) & 3u;
     if (kb < ns) start_round(kb);
-    for (; kb < ns; kb += WAVES * 64) {
+    while (kb < ns) {
+#if RHP_REPLAY_PRIO == 2
+      /* priorities rotated per round, out of step among the waves of a SIMD */
+      rp = (rp + 1u) & 3u;
+      switch (rp) {
+      case 0: __builtin_amdgcn_s_setprio(0); break;
+      case 1: __builtin_amdgcn_s_setprio(1); break;
+      case 2: __builtin_amdgcn_s_setprio(2); break;
+      default: __builtin_amdgcn_s_setprio(3);
+      }
+#endif
+      (void) rp;
+      const uint32_t kn = next_kb(kb);
       if constexpr (http) {
         dg.part_begin();
         while (__builtin_amdgcn_ballot_w64(w.live)) w.step();   /* what the last round's moves left */
@@ -2251,14 +2295,15 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         if (walking) mark_wide(p, wi);
         dg.part_end(4);
         const uint64_t m = __builtin_amdgcn_ballot_w64(staged);
-        if (kb + WAVES * 64 < ns) start_round(kb + WAVES * 64);
+        if (kn < ns) start_round(kn);
         else walking = w.live = false;
         dg.part_begin();
         if (m) staged_moves(m, sb, lane, stage, [&]() { w.step(); });
         dg.part_end(5);
       } else {
-        if (kb + WAVES * 64 < ns) start_round(kb + WAVES * 64);
+        if (kn < ns) start_round(kn);
       }
+      kb = kn;
     }
     dg.pass_end(0);
   }

@@ -17,7 +17,7 @@ NREQ = int(os.environ.get("STAMPS_N", 1 << 20))
 ONLY = os.environ.get("STAMPS_CFG")
 for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, rhp.LAYOUT_COMPACT),
                                       (rhp.GEN_ZIPF, 0x5EED0003, 32, 0, 0),
-                                      (rhp.GEN_POST1K, 0x5EED0005, 16, 1, 1), (rhp.GEN_CHUNKED, 0x5EED0006, 16, 1, 1)):
+                                      (rhp.GEN_POST1K, 0x5EED0005, 16, 1, rhp.LAYOUT_COMPACT), (rhp.GEN_CHUNKED, 0x5EED0006, 16, 1, 1)):
     if ONLY and str(cfg) not in ONLY.split(","):
         continue
     buf, off = rhp.generate(cfg, NREQ, seed)
@@ -89,3 +89,12 @@ for cfg, seed, maxh, mode, layout in ((rhp.GEN_GET256, 0x5EED0002, 16, 0, rhp.LA
         print(f"     pass 2 parts per wave: validation + serial paths {st[used, 22].mean():.0f} cycles, "
               f"staged moves {st[used, 23].mean():.0f} cycles")
     print(f"   workgroups: last wave's loop end {q(ends)}; first wave's {q(firsts)}", flush=True)
+    if (rt[:, 3] - rt[:, 4]).mean() > 50.0:   # a long replay (chunked): where its time goes
+        ex_last = np.array([rt[wg == g, 3].max() for g in np.unique(wg)])
+        ex_first = np.array([rt[wg == g, 3].min() for g in np.unique(wg)])
+        print(f"   workgroups: last wave's exit {q(ex_last)}; first wave's exit {q(ex_first)}")
+        print("   by wave slot: replay us (mean)")
+        print("     " + " ".join(f"{(rt[idx == k, 3] - rt[idx == k, 4]).mean():5.0f}" for k in range(16)))
+        ug = np.unique(wg)
+        print("   by XCD (workgroup mod 8): last wave's exit us (mean)")
+        print("     " + " ".join(f"{ex_last[(ug % 8) == x].mean():6.1f}" for x in range(8)), flush=True)

@@ -2263,29 +2263,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     uint32_t kb = claim();
     auto next_kb = [&](uint32_t) { return claim(); };
 #endif
-#if RHP_REPLAY_PRIO == 1
-    /* the waves a SIMD dispatched last at the higher priorities */
-    switch ((tid >> 8) & 3u) {
-    case 0: __builtin_amdgcn_s_setprio(0); break;
-    case 1: __builtin_amdgcn_s_setprio(1); break;
-    case 2: __builtin_amdgcn_s_setprio(2); break;
-    default: __builtin_amdgcn_s_setprio(3);
-    }
-#endif
-    uint32_t rp = (tid >> 8) & 3u;
     if (kb < ns) start_round(kb);
     while (kb < ns) {
-#if RHP_REPLAY_PRIO == 2
-      /* priorities rotated per round, out of step among the waves of a SIMD */
-      rp = (rp + 1u) & 3u;
-      switch (rp) {
-      case 0: __builtin_amdgcn_s_setprio(0); break;
-      case 1: __builtin_amdgcn_s_setprio(1); break;
-      case 2: __builtin_amdgcn_s_setprio(2); break;
-      default: __builtin_amdgcn_s_setprio(3);
-      }
-#endif
-      (void) rp;
       const uint32_t kn = next_kb(kb);
       if constexpr (http) {
         dg.part_begin();

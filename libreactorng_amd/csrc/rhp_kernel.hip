@@ -1846,11 +1846,13 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       issue();
     }
   } else {
-    /* the first windows, then the barrier that makes the pool area
-     * initialized before any wave's first refill */
+    /* the barrier that makes the table and the pool area initialized, then each
+     * wave's first windows: a wave enters the loop as soon as its own loads are
+     * issued, not when the slowest wave's are -- the first issue waits on a
+     * chip-wide burst of 32 MB (round 5: config 5 -3 %, config 2 +-0) */
+    __syncthreads();
     nw = pend_ok ? first_win(pend_o0) | 2u : 0u;
     issue();
-    __syncthreads();
   }
 
   /*

@@ -141,7 +141,8 @@ enum : uint32_t {
   kOrderSpan = 8192,
   kOrderBuckets = 64,                            /* window counts 1..63 (63: 63 or more) */
   kDeferCap = 480,                               /* the replay's list (defer) */
-  kPoolBytes = 4 * kPoolWords + 2 * kDeferCap
+  kPoolBytes = 4 * kPoolWords + 2 * kDeferCap,
+  kOrderWaves = 2                                /* idle waves whose staging holds an uneven range's order */
 };
 static_assert(idx2(S_DONE, 0) == kPark, "parked lanes sit in DONE");
 
@@ -1127,7 +1128,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   u32x4 W[kWParts];                    /* the window in registers */
   const uint32_t stage = __builtin_amdgcn_readfirstlane(kLdsTable + (tid >> 6) * kStageWave);   /* wave-uniform */
   /* the extension parts of the wave's windows (kXParts > 0): after the pool area */
-  const uint32_t xstage = __builtin_amdgcn_readfirstlane(kLdsTable + WAVES * kStageWave + kPoolBytes +
+  const uint32_t xstage = __builtin_amdgcn_readfirstlane(kLdsTable + WAVES * kStageWave + kPoolBytes + 4u * kOrderBuckets +
                                                          (tid >> 6) * 1024u * kXParts);
   /* the first window of the request starting at (low dword) o0, offset from
    * base, and the number of bytes before the request in it (see kLead) */
@@ -1178,9 +1179,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   };
   /* an uneven range's order: the range's requests (u16, range-relative) by
    * descending window count, then the histogram / bucket cursors */
-  uint16_t *order = reinterpret_cast<uint16_t *>(lds + kLdsTable + (WAVES - 3) * kStageWave);
-  uint32_t *bucket = reinterpret_cast<uint32_t *>(order + kOrderSpan);
-  static_assert(2 * kOrderSpan + 4 * kOrderBuckets <= 3 * kStageWave, "the order fits the last three waves' staging");
+  uint16_t *order = reinterpret_cast<uint16_t *>(lds + kLdsTable + (WAVES - kOrderWaves) * kStageWave);
+  uint32_t *bucket = reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave + kPoolBytes);   /* past the pool */
+  static_assert(2 * kOrderSpan <= kOrderWaves * kStageWave, "the order fits the last kOrderWaves waves' staging");
   auto refill_pend = [&]() {
     /* Just in time (early form, longest-first ranges): a lane takes its next
      * request only when its current one has at most two windows left -- the
@@ -1819,11 +1820,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * waves 398 us, 8 waves 474 us).  The other waves only join the barriers and
    * the replay. */
 #ifndef RHP_UNEVEN_WAVES
-#define RHP_UNEVEN_WAVES 12
+#define RHP_UNEVEN_WAVES 14
 #endif
   constexpr uint32_t kUnevenWaves = WAVES > RHP_UNEVEN_WAVES ? RHP_UNEVEN_WAVES : (uint32_t) WAVES;   /* 10: 472 us, 11: 450, 13: 408, 14: 413 */
-  /* the order lives in the last three waves' staging (sort_range): they must not walk */
-  static_assert(kUnevenWaves + 3u <= (uint32_t) WAVES, "the idle waves' staging holds the hand-out order");
+  /* the order lives in the last kOrderWaves waves' staging (sort_range): they must not walk */
+  static_assert(kUnevenWaves + kOrderWaves <= (uint32_t) WAVES, "the idle waves' staging holds the hand-out order");
   bool idle_wave = false;
   if (uneven) {
     /* the whole range longest first, the first hand-out included: a long
@@ -2363,7 +2364,8 @@ template <int WAVES, bool LATE, bool HTTP, bool COMPACT>
 int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
 {
   constexpr uint32_t kX = (LATE && HTTP) ? kHttpXParts : 0u;
-  const size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes + (size_t) WAVES * 1024u * kX;
+  const size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes + 4u * kOrderBuckets +
+                           (size_t) WAVES * 1024u * kX;
   static_assert(kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes + (size_t) WAVES * 1024u * kX <= 160u * 1024u,
                 "the workgroup's LDS fits the CU's 160 KiB");
   const uint64_t bit = 1ull << (8 * (WAVES / 4) + (COMPACT ? 4 : 0) + (LATE ? 2 : 0) + (HTTP ? 1 : 0));

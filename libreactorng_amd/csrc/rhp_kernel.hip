@@ -2207,12 +2207,12 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
     uint32_t wi = 0;
     int32_t wret = 0;
     bool walking = false;
-    auto start_round = [&](uint32_t kb) {
+    auto start_round = [&](uint32_t kb, uint32_t ke) {   /* entries [kb, ke), at most 64 */
       const uint32_t k = kb + lane;
       walking = false;
       w.live = false;
       dg.part_begin();
-      if (k < ns) {
+      if (k < ke) {
         uint32_t e, i;
         Head h;
         if (direct) {   /* the range in order: what the first pass would have done */
@@ -2248,27 +2248,27 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
      * (RHP_STAMPS, chunked: 500 vs 780 us for the same four rounds, the
      * workgroup's end set by its slowest wave), so the faster waves take more
      * rounds (round 5) */
-    uint32_t *round_next = wg_counter + 2;   /* 0 since the prologue */
-    auto claim = [&]() -> uint32_t {
-#ifdef RHP_STATIC_ROUNDS
-      static_cast<void>(round_next);
-      return 0u;
-#else
+    uint32_t *round_next = wg_counter + 2;   /* entries claimed; 0 since the prologue */
+    /* A round is at most 64 entries (one per lane).  Near the end of the range
+     * the rounds shrink (32, then 16 entries: RHP_TAIL_ROUNDS), so the last ones
+     * -- a 64-body round of chunked moves is ~150 us of one wave -- end closer
+     * together; a wave judges "near the end" from its own last claim */
+    auto claim = [&](uint32_t last) -> uint2 {
+      uint32_t want = 64u;
+#ifdef RHP_TAIL_ROUNDS
+      const uint32_t left = ns > last ? ns - last : 0u;
+      want = left > 32u * WAVES * 2u ? 64u : left > 16u * WAVES * 2u ? 32u : 16u;
+#endif
+      (void) last;
       uint32_t r = 0;
-      if (lane == 0) r = atomicAdd(round_next, 1u);
-      return 64u * __builtin_amdgcn_readfirstlane(r);
-#endif
+      if (lane == 0) r = atomicAdd(round_next, want);
+      r = __builtin_amdgcn_readfirstlane(r);
+      return uint2{r, min(r + want, ns)};
     };
-#ifdef RHP_STATIC_ROUNDS
-    uint32_t kb = tid & ~63u;
-    auto next_kb = [&](uint32_t k) { return k + WAVES * 64; };
-#else
-    uint32_t kb = claim();
-    auto next_kb = [&](uint32_t) { return claim(); };
-#endif
-    if (kb < ns) start_round(kb);
-    while (kb < ns) {
-      const uint32_t kn = next_kb(kb);
+    uint2 kr = claim(0u);
+    if (kr.x < ns) start_round(kr.x, kr.y);
+    while (kr.x < ns) {
+      const uint2 kn = claim(kr.y);
       if constexpr (http) {
         dg.part_begin();
         while (__builtin_amdgcn_ballot_w64(w.live)) w.step();   /* what the last round's moves left */
@@ -2277,15 +2277,15 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         if (walking) mark_wide(p, wi);
         dg.part_end(4);
         const uint64_t m = __builtin_amdgcn_ballot_w64(staged);
-        if (kn < ns) start_round(kn);
+        if (kn.x < ns) start_round(kn.x, kn.y);
         else walking = w.live = false;
         dg.part_begin();
         if (m) staged_moves(m, sb, lane, stage, [&]() { w.step(); });
         dg.part_end(5);
       } else {
-        if (kn < ns) start_round(kn);
+        if (kn.x < ns) start_round(kn.x, kn.y);
       }
-      kb = kn;
+      kr = kn;
     }
     dg.pass_end(0);
   }

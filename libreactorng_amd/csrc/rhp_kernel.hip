@@ -1813,16 +1813,15 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   const bool uneven =
       may_order && __builtin_amdgcn_ballot_w64((uint64_t) (s1 - s0) * span_n > 2u * (o_hi - o_lo)) != 0;
   wt = p.wt_records && !uneven;
-  /* An uneven range runs on 12 of the 16 waves: its end is set by its longest
-   * requests (each walked by one lane from the first iteration on), and with
-   * fewer waves sharing the CU every iteration is shorter while the lanes'
-   * share of the rest still fits beside them (config 3: 16 waves 422 us, 12
-   * waves 398 us, 8 waves 474 us).  The other waves only join the barriers and
-   * the replay. */
+  /* An uneven range runs on 14 of the 16 waves (the other two hold the
+   * hand-out order in their staging and only join the barriers and the replay).
+   * Round 3, traffic-bound with 4-aligned windows: 16 waves 422 us, 12 waves 398
+   * us, 8 waves 474 us; round 5, after line windows the loop is latency-bound and
+   * more waves pay again: 12 waves 282 us, 13: 278, 14: 277 (profiles/r05/config3/). */
 #ifndef RHP_UNEVEN_WAVES
 #define RHP_UNEVEN_WAVES 14
 #endif
-  constexpr uint32_t kUnevenWaves = WAVES > RHP_UNEVEN_WAVES ? RHP_UNEVEN_WAVES : (uint32_t) WAVES;   /* 10: 472 us, 11: 450, 13: 408, 14: 413 */
+  constexpr uint32_t kUnevenWaves = WAVES > RHP_UNEVEN_WAVES ? RHP_UNEVEN_WAVES : (uint32_t) WAVES;
   /* the order lives in the last kOrderWaves waves' staging (sort_range): they must not walk */
   static_assert(kUnevenWaves + kOrderWaves <= (uint32_t) WAVES, "the idle waves' staging holds the hand-out order");
   bool idle_wave = false;

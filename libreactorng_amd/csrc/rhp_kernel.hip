@@ -1179,7 +1179,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   };
   /* an uneven range's order: the range's requests (u16, range-relative) by
    * descending window count, then the histogram / bucket cursors */
-  uint16_t *order = reinterpret_cast<uint16_t *>(lds + kLdsTable + (WAVES - kOrderWaves) * kStageWave);
+  /* in the last waves' staging: one wave's for a range of up to kStageWave / 2
+   * requests (config 3 at 1M: 4096 per workgroup), two waves' up to kOrderSpan */
+  const uint32_t order_waves = 2u * (wg_hi - wg_lo) <= kStageWave ? 1u : kOrderWaves;
+  uint16_t *order = reinterpret_cast<uint16_t *>(lds + kLdsTable + (WAVES - order_waves) * kStageWave);
   uint32_t *bucket = reinterpret_cast<uint32_t *>(lds + kLdsTable + WAVES * kStageWave + kPoolBytes);   /* past the pool */
   static_assert(2 * kOrderSpan <= kOrderWaves * kStageWave, "the order fits the last kOrderWaves waves' staging");
   auto refill_pend = [&]() {
@@ -1813,17 +1816,18 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   const bool uneven =
       may_order && __builtin_amdgcn_ballot_w64((uint64_t) (s1 - s0) * span_n > 2u * (o_hi - o_lo)) != 0;
   wt = p.wt_records && !uneven;
-  /* An uneven range runs on 14 of the 16 waves (the other two hold the
-   * hand-out order in their staging and only join the barriers and the replay).
+  /* An uneven range runs on 15 of the 16 waves (14 when its order needs two
+   * waves' staging; the others hold the hand-out order and only join the
+   * barriers and the replay).
    * Round 3, traffic-bound with 4-aligned windows: 16 waves 422 us, 12 waves 398
    * us, 8 waves 474 us; round 5, after line windows the loop is latency-bound and
    * more waves pay again: 12 waves 282 us, 13: 278, 14: 277 (profiles/r05/config3/). */
 #ifndef RHP_UNEVEN_WAVES
-#define RHP_UNEVEN_WAVES 14
+#define RHP_UNEVEN_WAVES 15
 #endif
   constexpr uint32_t kUnevenWaves = WAVES > RHP_UNEVEN_WAVES ? RHP_UNEVEN_WAVES : (uint32_t) WAVES;
   /* the order lives in the last kOrderWaves waves' staging (sort_range): they must not walk */
-  static_assert(kUnevenWaves + kOrderWaves <= (uint32_t) WAVES, "the idle waves' staging holds the hand-out order");
+  static_assert(kUnevenWaves + 1u <= (uint32_t) WAVES, "an idle wave's staging holds the hand-out order");
   bool idle_wave = false;
   if (uneven) {
     /* the whole range longest first, the first hand-out included: a long
@@ -1833,7 +1837,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
      * reset before the first refill) */
     pend_ok = false;
     sorted = true;
-    idle_wave = (tid >> 6) >= kUnevenWaves;
+    idle_wave = (tid >> 6) >= min(kUnevenWaves, (uint32_t) WAVES - order_waves);
     if (tid < kOrderBuckets) bucket[tid] = 0u;
     __syncthreads();
     if (tid == 0) *wg_counter = 0;

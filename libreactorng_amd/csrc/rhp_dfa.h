@@ -308,11 +308,12 @@ RHP_DHD constexpr uint32_t state2(uint32_t idx)
  * stride of 256 the walk's address is one v_perm (idx * 256 + code), and every
  * row starts in LDS bank 0: lanes in different states reading the same code
  * read the same bank at different addresses, an N-way conflict in the walk's
- * dependent read.  A stride of 260 (RHP_ROW_STRIDE) starts row idx one bank
- * further (one v_mad_u32_u24 instead of the v_perm).
+ * dependent read.  A stride of 256 + 4k (RHP_ROW_STRIDE; 268: k = 3) starts row
+ * idx k banks further (one v_mad_u32_u24 instead of the v_perm).
  */
 #ifndef RHP_ROW_STRIDE
-#define RHP_ROW_STRIDE 260   /* round 5: after line windows 1-2 % faster on configs 2/3/5 (profiles/r05/ab/) */
+#define RHP_ROW_STRIDE 268   /* round 5: rows 3 banks apart; 260 (1 bank) after line windows was 1-2 % faster
+                                than 256 on configs 2/3/5, 268 another 2.7 % on config 5 (profiles/r05/ab/) */
 #endif
 enum : uint32_t {
   kStride = RHP_ROW_STRIDE,

@@ -72,3 +72,28 @@ def test_gpu_line_windows_vs_oracle_and_emulator(maxh):
             assert_same(canon(res, rhp.MODE_PHR), want, buf, off, f"GPU line windows impl{impl} maxh {maxh}")
             assert np.array_equal(res.reqs["flags"] & (rhp.F_EXACT | rhp.F_WIDE),
                                   emu.reqs["flags"] & (rhp.F_EXACT | rhp.F_WIDE)), (impl, layout)
+
+
+def uneven_large_batch(n=1_300_000, seed=21):
+    """Ranges of 4096-8192 requests (n / 256 CUs) whose first requests are longer
+    than twice the range's mean: the longest-first hand-out with its order in
+    the last TWO waves' staging (rhp_kernel.hip order_waves; 1M-request config 3
+    ranges take one wave's).  Every 8th request carries 30 header lines, the
+    rest are short; request starts fall at every lead."""
+    rng = np.random.default_rng(seed)
+    short = [b"GET /a HTTP/1.1\r\nH: v\r\n\r\n", b"POST /b HTTP/1.0\r\nA: 1\r\nB: 2\r\n\r\n", b"GET / HTTP/1.1\r\n\r\n"]
+    long = b"GET /" + b"p" * 37 + b" HTTP/1.1\r\n" + b"".join(b"X-H%02d: %s\r\n" % (k, b"v" * (k % 7)) for k in range(30)) + b"\r\n"
+    pick = rng.integers(0, len(short), n)
+    reqs = [long if i % 8 == 0 else short[pick[i]] for i in range(n)]
+    return pack(reqs)
+
+
+@pytest.mark.gpu
+def test_gpu_uneven_ranges_with_two_order_waves():
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    buf, off = uneven_large_batch(n=cus * 5000)
+    assert 4096 < (len(off) - 1) // cus <= 8192
+    want = to_rhp(*run_oracle(buf, off, 32, rhp.MODE_PHR)[:3], rhp.MODE_PHR)
+    res = rhp.parse_batch(buf, off, 32, rhp.MODE_PHR)
+    assert_same(canon(res, rhp.MODE_PHR), want, buf, off, "GPU uneven ranges, two order waves")

@@ -1,0 +1,14 @@
+#!/bin/bash
+# round 5 session af: issue priority by remaining work once the pool is dry (tp)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT}" && mkdir -p gpurun_out/r5ak && export TMPDIR=/tmp
+L=$PWD/libreactorng_amd
+for r in 1 2 3; do
+  for v in cur tp; do
+    for c in get256 zipf post; do
+      RHP_LIB=$L/librhp_x_$v.so timeout -k 10 300 python bench.py --config $c --extra none --no-cpu --no-e2e --steps 30 --warmup 5 > gpurun_out/r5ak/${c}_$v.json 2>/dev/null || exit 1
+      python3 -c "import json; d=json.load(open('gpurun_out/r5ak/${c}_$v.json')); print('$v', '$c', round(d['roofline']['kernel_ms']*1e3,1), 'us', d['parity'])" | tee -a gpurun_out/r5ak/ab.txt
+    done
+  done
+done
+echo SESSION_OK

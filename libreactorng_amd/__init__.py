@@ -32,6 +32,7 @@ IMPL_DFA, IMPL_EXACT, IMPL_DFA_LATE = 0, 1, 2
 RHP_NAME_NULL = 0xFFFF
 F_EXACT = 0x1
 F_WIDE = 0x2   # compact layout: the request's header records are in the wide area (rhp.h)
+HTTP_WIDE = 0x1   # compact http records (rhp_http_compact_t.flags): the record is in the wide area (rhp.h)
 
 GEN_TFB128, GEN_GET256, GEN_ZIPF, GEN_POST1K, GEN_CHUNKED, GEN_FUZZ, GEN_FUZZ_HTTP = 1, 2, 3, 5, 6, 100, 101
 
@@ -82,17 +83,60 @@ class RespBatch(ctypes.Structure):
 RHP_DATE_LEN = 29
 
 
+def _torch_hip_runtime() -> str | None:
+    """Path of the HIP runtime torch ships (torch/lib/libamdhip64.so), found
+    without importing torch."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return None
+    path = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    return path if os.path.exists(path) else None
+
+
+def hip_runtimes() -> list[str]:
+    """The libamdhip64 files mapped into this process (Linux /proc/self/maps)."""
+    try:
+        with open("/proc/self/maps") as f:
+            return sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln and "/" in ln})
+    except OSError:
+        return []
+
+
+def check_one_hip_runtime() -> None:
+    """Two HIP runtimes in one process (torch's and /opt/rocm's) each own their
+    device memory: a kernel of one launched on buffers of the other fails with
+    error 100.  Raise with the cause instead."""
+    rt = [os.path.realpath(p) for p in hip_runtimes()]
+    if len(set(rt)) > 1:
+        raise RuntimeError("two HIP runtimes are loaded (" + ", ".join(sorted(set(rt))) + "): librhp.so was "
+                           "loaded before torch without libreactorng_amd.lib(); load it through lib(), or "
+                           "import torch first")
+
+
 def lib() -> ctypes.CDLL:
-    """librhp.so (HIP).  Raises if it is missing: there is no fallback."""
+    """librhp.so (HIP).  Raises if it is missing: there is no fallback.
+
+    Load order.  librhp.so's DT_NEEDED is libamdhip64.so.7 (the
+    soname of both /opt/rocm's runtime and the one torch ships); torch's
+    libc10_hip.so asks for the unversioned libamdhip64.so through its $ORIGIN
+    rpath.  ld.so reuses a loaded library only when a request matches its soname
+    or the name it was loaded by, so torch-first gives one runtime (librhp's
+    request matches the soname of torch's copy), while librhp-first loads
+    /opt/rocm's copy and torch's later request for `libamdhip64.so` matches
+    neither name: torch then loads its own copy, and tensors it allocates are
+    foreign to librhp's runtime.  So torch's runtime, when torch is installed, is
+    preloaded by path (RTLD_GLOBAL) before librhp.so, without importing torch;
+    a process without torch uses /opt/rocm's."""
     global _rhp
     if _rhp is None:
         if not os.path.exists(LIBRHP):
             raise RuntimeError(f"{LIBRHP} missing: run __graft_entry__.build() (hipcc gfx950)")
-        try:   # torch first: its HIP runtime is then the one librhp.so binds to (one runtime per process;
-            import torch  # noqa: F401  loading librhp.so first made torch's device buffers foreign to it: error 100)
-        except ImportError:
-            pass
+        rt = _torch_hip_runtime()
+        if rt is not None:
+            ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
         _rhp = ctypes.CDLL(LIBRHP)
+        check_one_hip_runtime()
         _rhp.rhp_parse_batch.argtypes = [ctypes.POINTER(Batch), ctypes.c_void_p]
         _rhp.rhp_parse_batch.restype = ctypes.c_int
         _rhp.rhp_set_impl.argtypes = [ctypes.c_int]
@@ -406,6 +450,7 @@ class DeviceBatch:
         import torch
         s = stream if stream is not None else torch.cuda.current_stream()
         d = self.desc()
+        check_one_hip_runtime()
         rc = lib().rhp_parse_batch(ctypes.byref(d), ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
             raise RuntimeError(f"rhp_parse_batch failed: {rc}")

@@ -598,12 +598,20 @@ void reactor_batch_result(int k, reactor_batch_result_t *out)
     enum { MAX_RUNS = 16 };
     uint64_t run_lo[MAX_RUNS], run_hi[MAX_RUNS], span_lo = 0, span_hi = 0;
     uint32_t runs = 0;
-    for (uint32_t i = 0; i < s->n; i++)
+    /* only the record slots the fix-up filled: slots [piece_lo, piece_lo +
+     * n_slots) of each session (the slots after them keep the
+     * speculative records, whose req_start is whatever the device buffer held);
+     * the ranges are clamped to the round's bytes */
+    for (uint32_t q = 0; q < s->n_sess; q++)
+    for (uint32_t i = s->h_sess[q].piece_lo; i < s->h_sess[q].piece_lo + s->h_sres[q].n_slots && i < s->n; i++)
     {
       const rhp_http_t *x = &s->h_http[i];
       if (!(x->result == 1 && x->body_kind && x->consumed != (uint64_t) s->h_req[i].ret + x->body_len))
         continue;
-      const uint64_t a = s->h_start[i], b = a + x->consumed;
+      const uint64_t a = s->h_start[i] < s->bytes ? s->h_start[i] : s->bytes;
+      const uint64_t b = x->consumed < s->bytes - a ? a + x->consumed : s->bytes;
+      if (b <= a)
+        continue;
       span_lo = runs && span_lo < a ? span_lo : a;
       span_hi = b > span_hi ? b : span_hi;
       if (runs && runs <= MAX_RUNS && a <= run_hi[runs - 1])

@@ -379,7 +379,9 @@ extern "C" int rhp_cpu_fixup_sessions(const rhp_batch_t *b, const rhp_session_t 
 /* The exact scalar path alone, on the host (the product's CPU parser). */
 extern "C" int rhp_cpu_parse_batch(const rhp_batch_t *b)
 {
-  if (b->layout == RHP_LAYOUT_COMPACT && b->mode != RHP_MODE_PHR) return -22;   /* as rhp_parse_batch */
+  /* as rhp_parse_batch: compact records in both modes (every record wide: the
+   * exact path's), not in a speculative batch */
+  if (b->layout == RHP_LAYOUT_COMPACT && (b->flags & RHP_BATCH_SPECULATIVE)) return -22;
   for (uint32_t i = 0; i < b->n; i++) emu_exact(b, i, b->offsets[i], b->offsets[i + 1] - b->offsets[i]);
   return 0;
 }

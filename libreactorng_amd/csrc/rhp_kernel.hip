@@ -1825,8 +1825,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 #ifndef RHP_UNEVEN_WAVES
 #define RHP_UNEVEN_WAVES 15
 #endif
-  constexpr uint32_t kUnevenWaves = WAVES > RHP_UNEVEN_WAVES ? RHP_UNEVEN_WAVES : (uint32_t) WAVES;
-  /* the order lives in the last kOrderWaves waves' staging (sort_range): they must not walk */
+  /* the order lives in the last order_waves waves' staging (sort_range): they
+   * must not walk, so at least one wave stays idle whatever the knobs (the http
+   * instance has fewer waves with RHP_HTTP_XPARTS > 0) */
+  constexpr uint32_t kUnevenWaves = (uint32_t) WAVES - 1u < (uint32_t) RHP_UNEVEN_WAVES ? (uint32_t) WAVES - 1u
+                                                                                     : (uint32_t) RHP_UNEVEN_WAVES;
   static_assert(kUnevenWaves + 1u <= (uint32_t) WAVES, "an idle wave's staging holds the hand-out order");
   bool idle_wave = false;
   if (uneven) {
@@ -2367,10 +2370,11 @@ template <int WAVES, bool LATE, bool HTTP, bool COMPACT>
 int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
 {
   constexpr uint32_t kX = (LATE && HTTP) ? kHttpXParts : 0u;
-  const size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes + 4u * kOrderBuckets +
-                           (size_t) WAVES * 1024u * kX;
-  static_assert(kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes + (size_t) WAVES * 1024u * kX <= 160u * 1024u,
-                "the workgroup's LDS fits the CU's 160 KiB");
+  /* table, staging, pool area, the order's bucket cursors past it (the kernel's
+   * `bucket`), the extension parts: one sum for the launch and the check */
+  constexpr size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes + 4u * kOrderBuckets +
+                               (size_t) WAVES * 1024u * kX;
+  static_assert(lds_bytes <= 160u * 1024u, "the workgroup's LDS fits the CU's 160 KiB");
   const uint64_t bit = 1ull << (8 * (WAVES / 4) + (COMPACT ? 4 : 0) + (LATE ? 2 : 0) + (HTTP ? 1 : 0));
   if (!(g_attr[dev].load(std::memory_order_acquire) & bit)) {
     /* idempotent: two threads of one device may both set it */

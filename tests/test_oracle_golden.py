@@ -59,10 +59,13 @@ def test_cpu_exact_parser_matches_golden(name):
     spec, buf, off, want, z = load_golden(name)
     res = rhp.parse_cpu_exact(buf, off, spec["max_headers"], spec["mode"], rhp.LAYOUT_HEADER_MAJOR)
     assert_same(canon(res, spec["mode"]), want, buf, off, f"CPU exact parser vs golden {name}")
-    if spec["mode"] == rhp.MODE_PHR:   # compact layout: every record wide (RHP_F_WIDE), expanded the same
-        res = rhp.parse_cpu_exact(buf, off, spec["max_headers"], spec["mode"], rhp.LAYOUT_COMPACT)
-        assert_same(canon(res, spec["mode"]), want, buf, off, f"CPU exact parser (compact) vs golden {name}")
-        assert ((res.reqs["flags"] & rhp.F_WIDE) != 0).all()
+    # compact layout (phr and, ADVICE r5, http records): every record wide (RHP_F_WIDE), expanded the same
+    res = rhp.parse_cpu_exact(buf, off, spec["max_headers"], spec["mode"], rhp.LAYOUT_COMPACT)
+    assert_same(canon(res, spec["mode"]), want, buf, off, f"CPU exact parser (compact) vs golden {name}")
+    assert ((res.reqs["flags"] & rhp.F_WIDE) != 0).all()
+    if spec["mode"] == rhp.MODE_HTTP:
+        hc = res.raw_http[: 8 * (len(off) - 1)].view(np.uint8).reshape(-1, 8)
+        assert (hc[:, 2] & rhp.HTTP_WIDE).all(), "every compact http record of the exact path is wide"
 
 
 def vectors():

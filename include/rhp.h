@@ -81,8 +81,9 @@ typedef struct rhp_hdr {
 enum rhp_layout {
   RHP_LAYOUT_REQUEST_MAJOR = 0,
   RHP_LAYOUT_HEADER_MAJOR = 1,
-  RHP_LAYOUT_COMPACT = 2      /* 4-byte header records, below (http mode: 8-byte http records too;
+  RHP_LAYOUT_COMPACT = 2,     /* 4-byte header records, below (http mode: 8-byte http records too;
                                  not with RHP_BATCH_SPECULATIVE) */
+  RHP_LAYOUT_DENSE = 3        /* RHP_MODE_PHR: 8-byte request and 2-byte header records, below */
 };
 /* Compact records (RHP_LAYOUT_COMPACT).  A header line the DFA
  * parses is `name ": " value CRLF` and the first one starts right after the
@@ -101,6 +102,37 @@ enum rhp_layout {
  * 2: 48 -> 32 B per request with the 16-B request record). */
 #define RHP_COMPACT_WIDE_OFF(n, m) ((((size_t) (n) * (size_t) (m) * 4u) + 15u) & ~(size_t) 15u)
 #define RHP_COMPACT_HDRS_BYTES(n, m) (RHP_COMPACT_WIDE_OFF(n, m) + (size_t) (n) * (size_t) (m) * 8u)
+/* Dense records (RHP_LAYOUT_DENSE, RHP_MODE_PHR; round 6).  The compact
+ * layout's running-sum offsets with narrower fields, for the DFA's records.
+ * reqs holds rhp_req_dense_t dreq[n] (8 B) and, at byte
+ * RHP_DENSE_REQ_WIDE_OFF(n), a wide area rhp_req_t wide[n]
+ * (RHP_DENSE_REQS_BYTES(n) bytes in all); hdrs holds u16 lens[max_headers][n]
+ * (header-major), name_len | value_len << 6, and at byte RHP_DENSE_WIDE_OFF(n, m)
+ * the wide header records rhp_hdr_t wide[n][m] (RHP_DENSE_HDRS_BYTES(n, m)).
+ * A DFA record is dense when it fits: method_len <= 255 (path_off = method_len
+ * + 1, method_off = 0), every header name < 63 and value < 1008 bytes; any other
+ * request (those, and every request the exact path parses) is wide: dreq[i].flags
+ * holds RHP_DENSE_WIDE and its records are wide[i] and the wide header records.
+ * RHP_DENSE_BAD: ret = -1 (the other outputs unspecified, as in rhp_req_t).
+ * Config 2 writes 8 + 4 x 2 = 16 B of records per request (compact: 32 B).
+ * rhp_expand_reqs / rhp_expand_records (rhp_host.h) expand them on the host. */
+typedef struct rhp_req_dense {
+  uint16_t ret;           /* 1..65535 (the header section), when neither flag is set */
+  uint16_t path_len;
+  uint8_t  method_len;
+  uint8_t  num_headers;
+  uint8_t  minor_version;
+  uint8_t  flags;         /* RHP_DENSE_WIDE, RHP_DENSE_BAD */
+} rhp_req_dense_t;
+#define RHP_DENSE_WIDE 1u
+#define RHP_DENSE_BAD  2u
+#define RHP_DENSE_NAME_MAX 62u    /* longest name a dense header record holds */
+#define RHP_DENSE_VALUE_MAX 1007u /* longest value */
+#define RHP_DENSE_REQ_WIDE_OFF(n) ((((size_t) (n) * 8u) + 15u) & ~(size_t) 15u)
+#define RHP_DENSE_REQS_BYTES(n) (RHP_DENSE_REQ_WIDE_OFF(n) + (size_t) (n) * 16u)
+#define RHP_DENSE_WIDE_OFF(n, m) ((((size_t) (n) * (size_t) (m) * 2u) + 15u) & ~(size_t) 15u)
+#define RHP_DENSE_HDRS_BYTES(n, m) (RHP_DENSE_WIDE_OFF(n, m) + (size_t) (n) * (size_t) (m) * 8u)
+
 /* record k of request i in a batch of n requests with capacity m */
 #define RHP_HDR(hdrs, layout, n, m, i, k) \
   ((hdrs)[(layout) == RHP_LAYOUT_HEADER_MAJOR ? (size_t) (k) * (n) + (i) : (size_t) (i) * (m) + (k)])
@@ -150,10 +182,12 @@ typedef struct rhp_batch {
   uint32_t        max_headers; /* headers capacity per request (*num_headers in) */
   uint32_t        mode;        /* enum rhp_mode */
   uint32_t        layout;      /* enum rhp_layout: where record k of request i lives in hdrs */
-  rhp_req_t      *reqs;        /* device [n] */
+  rhp_req_t      *reqs;        /* device [n] (RHP_LAYOUT_DENSE: RHP_DENSE_REQS_BYTES(n) bytes,
+                                  rhp_req_dense_t and the wide area) */
   rhp_hdr_t      *hdrs;        /* device [n * max_headers] records, laid out as `layout` says
                                   (n * max_headers < 2^32); RHP_LAYOUT_COMPACT:
-                                  RHP_COMPACT_HDRS_BYTES(n, max_headers) bytes */
+                                  RHP_COMPACT_HDRS_BYTES(n, max_headers) bytes; RHP_LAYOUT_DENSE:
+                                  RHP_DENSE_HDRS_BYTES(n, max_headers) bytes */
   rhp_http_t     *http;        /* device [n], RHP_MODE_HTTP (RHP_LAYOUT_COMPACT:
                                   RHP_COMPACT_HTTP_BYTES(n) bytes, rhp_http_compact_t) */
   uint32_t       *work;        /* reserved, may be NULL (device scratch of RHP_WORK_WORDS u32

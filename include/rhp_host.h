@@ -8,8 +8,9 @@
  *   rhp_emu_parse_batch   CPU emulation of the kernel's DFA algorithm, block for
  *                         block (tests only); stats[3] = fast ok, fast -1, exact
  *   (both take an rhp_batch_t (include/rhp.h) whose pointers are host memory)
- *   rhp_expand_records    any layout's header records (the compact ones
- *                         included) as rhp_hdr_t, on the host
+ *   rhp_expand_records    any layout's header records (the compact and dense
+ *                         ones included) as rhp_hdr_t, on the host;
+ *   rhp_expand_reqs       the dense layout's request records as rhp_req_t
  *
  *   rhp_phr_parse_request the same exact parser with phr_parse_request's own
  *                         signature and outputs (pointers into buf, no length
@@ -41,10 +42,17 @@ int rhp_emu_parse_batch(const rhp_batch_t *batch, uint64_t *stats);
 /* A parsed batch's header records as rhp_hdr_t, out[i * max_headers + k]
  * (request-major), from host copies of its reqs and hdrs in the batch's
  * layout; records past num_headers and those of requests with ret <= 0 are
- * zeroed.  For RHP_LAYOUT_COMPACT this is the running sum of rhp.h (the wide
- * records for RHP_F_WIDE requests).  `batch` supplies n, max_headers and
+ * zeroed.  For RHP_LAYOUT_COMPACT / RHP_LAYOUT_DENSE this is the running sum
+ * of rhp.h (the wide records for RHP_F_WIDE requests; reqs as rhp_expand_reqs
+ * makes them).  `batch` supplies n, max_headers and
  * layout only.  0, or -22 on bad arguments. */
 int rhp_expand_records(const rhp_batch_t *batch, const rhp_req_t *reqs, const void *hdrs, rhp_hdr_t *out);
+/* A parsed batch's request records as rhp_req_t[n]: copied, or for
+ * RHP_LAYOUT_DENSE expanded from rhp_req_dense_t and the wide area (rhp.h;
+ * a dense record's flags become 0, a wide one's RHP_F_WIDE is set).  `reqs` is
+ * the batch's reqs buffer as the parser left it.  0, or -22.  Expand the
+ * requests first: rhp_expand_records and rhp_expand_http take rhp_req_t. */
+int rhp_expand_reqs(const rhp_batch_t *batch, const void *reqs, rhp_req_t *out);
 /* A batch's http records (RHP_MODE_HTTP) as rhp_http_t[n]: copied, or for
  * RHP_LAYOUT_COMPACT expanded from the compact records and their wide area
  * (rhp.h rhp_http_compact_t; consumed from reqs[i].ret).  0, or -22. */

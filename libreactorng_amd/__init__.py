@@ -27,12 +27,13 @@ RHP_MAX_HEADERS = 64
 RHP_RET_TOOLONG = -3
 RHP_WORK_WORDS = 64
 MODE_PHR, MODE_HTTP = 0, 1
-LAYOUT_REQUEST_MAJOR, LAYOUT_HEADER_MAJOR, LAYOUT_COMPACT = 0, 1, 2
+LAYOUT_REQUEST_MAJOR, LAYOUT_HEADER_MAJOR, LAYOUT_COMPACT, LAYOUT_DENSE = 0, 1, 2, 3
 IMPL_DFA, IMPL_EXACT, IMPL_DFA_LATE = 0, 1, 2
 RHP_NAME_NULL = 0xFFFF
 F_EXACT = 0x1
 F_WIDE = 0x2   # compact layout: the request's header records are in the wide area (rhp.h)
 HTTP_WIDE = 0x1   # compact http records (rhp_http_compact_t.flags): the record is in the wide area (rhp.h)
+DENSE_WIDE, DENSE_BAD = 0x1, 0x2   # dense request records (rhp_req_dense_t.flags, rhp.h)
 
 GEN_TFB128, GEN_GET256, GEN_ZIPF, GEN_POST1K, GEN_CHUNKED, GEN_FUZZ, GEN_FUZZ_HTTP = 1, 2, 3, 5, 6, 100, 101
 
@@ -65,7 +66,7 @@ RHP_SYMBOLS = ("rhp_parse_batch", "rhp_set_impl", "rhp_kernel_name", "rhp_versio
                "rhp_fixup_sessions")
 HOST_SYMBOLS = ("rhp_gen_size", "rhp_gen_fill", "rhp_gen_header_bytes", "rhp_splitmix64",
                 "rhp_emu_parse_batch", "rhp_cpu_parse_batch", "rhp_phr_parse_request", "rhp_http_read_cpu",
-                "rhp_cpu_fixup_sessions", "rhp_expand_records", "rhp_expand_http", "rhp_test_chunk_window",
+                "rhp_cpu_fixup_sessions", "rhp_expand_records", "rhp_expand_http", "rhp_expand_reqs", "rhp_test_chunk_window",
                 "rhp_test_chunk_exact")
 
 _rhp = None
@@ -178,6 +179,8 @@ def host() -> ctypes.CDLL:
         _host.rhp_expand_records.argtypes = [ctypes.POINTER(Batch), vp, vp, vp]
         _host.rhp_expand_records.restype = ctypes.c_int
         _host.rhp_expand_http.argtypes = [ctypes.POINTER(Batch), vp, vp, vp]
+        _host.rhp_expand_reqs.argtypes = [ctypes.POINTER(Batch), vp, vp]
+        _host.rhp_expand_reqs.restype = ctypes.c_int
         _host.rhp_expand_http.restype = ctypes.c_int
     return _host
 
@@ -261,6 +264,7 @@ class Result:
     bytes_out: np.ndarray | None = None  # request bytes after http mode (chunked bodies rewritten)
     raw_hdrs: np.ndarray | None = None   # the hdrs buffer as the parser left it (its layout's bytes)
     raw_http: np.ndarray | None = None   # the http buffer as the parser left it (compact: rhp_http_compact_t)
+    raw_reqs: np.ndarray | None = None   # the reqs buffer as the parser left it (dense: rhp_req_dense_t + wide)
 
 
 def canonical(res: Result, mode: int):
@@ -315,10 +319,35 @@ def library_sha256(path: str | None = None) -> str:
 
 
 def hdrs_bytes(n: int, max_headers: int, layout: int) -> int:
-    """bytes the batch's hdrs buffer needs (rhp.h; RHP_COMPACT_HDRS_BYTES for the compact layout)"""
+    """bytes the batch's hdrs buffer needs (rhp.h; RHP_COMPACT_HDRS_BYTES / RHP_DENSE_HDRS_BYTES)"""
     if layout == LAYOUT_COMPACT:
         return ((n * max_headers * 4 + 15) & ~15) + n * max_headers * HDR_DTYPE.itemsize
+    if layout == LAYOUT_DENSE:
+        return ((n * max_headers * 2 + 15) & ~15) + n * max_headers * HDR_DTYPE.itemsize
     return n * max_headers * HDR_DTYPE.itemsize
+
+
+def reqs_bytes(n: int, layout: int) -> int:
+    """bytes the batch's reqs buffer needs (rhp.h; RHP_DENSE_REQS_BYTES for the dense layout)"""
+    if layout == LAYOUT_DENSE:
+        return ((n * 8 + 15) & ~15) + n * REQ_DTYPE.itemsize
+    return n * REQ_DTYPE.itemsize
+
+
+def expand_reqs(raw: np.ndarray, n: int, layout: int) -> np.ndarray:
+    """[n] rhp_req_t records of a parsed batch from its raw reqs bytes in any layout
+    (rhp_expand_reqs, include/rhp_host.h: dense records expanded)."""
+    raw = np.ascontiguousarray(raw).view(np.uint8)
+    if layout != LAYOUT_DENSE:
+        return raw[: n * REQ_DTYPE.itemsize].view(REQ_DTYPE).copy()
+    out = np.zeros(n, dtype=REQ_DTYPE)
+    if n == 0:
+        return out
+    b = Batch(None, None, None, 0, n, 0, MODE_PHR, layout, None, None, None, None, 0, 0, None)
+    rc = host().rhp_expand_reqs(ctypes.byref(b), _ptr(raw), _ptr(out))
+    if rc != 0:
+        raise RuntimeError(f"rhp_expand_reqs failed: {rc}")
+    return out
 
 
 def http_bytes(n: int, mode: int, layout: int) -> int:
@@ -372,21 +401,25 @@ def hdr_view(flat: np.ndarray, n: int, max_headers: int, layout: int) -> np.ndar
 
 def _host_batch(buf, off, max_headers, mode, layout=LAYOUT_REQUEST_MAJOR, last_len=None, flags=0):
     n = len(off) - 1
-    reqs = np.zeros(n, dtype=REQ_DTYPE)
+    raw_reqs = np.zeros(max(reqs_bytes(n, layout), 8), dtype=np.uint8)
+    reqs = raw_reqs[: n * REQ_DTYPE.itemsize].view(REQ_DTYPE)   # (dense: expanded by _host_done)
     raw = np.zeros(max(hdrs_bytes(n, max_headers, layout), 8), dtype=np.uint8)
     raw_http = np.zeros(max(http_bytes(n, mode, layout), 8), dtype=np.uint8)
     rw = buf.copy()
-    b = Batch(_ptr(rw), _ptr(rw), _ptr(off), rw.size, n, max_headers, mode, layout, _ptr(reqs), _ptr(raw),
+    b = Batch(_ptr(rw), _ptr(rw), _ptr(off), rw.size, n, max_headers, mode, layout, _ptr(raw_reqs), _ptr(raw),
               _ptr(raw_http), 0, flags, 0, _ptr(last_len) if last_len is not None else None)
-    hv = None if layout == LAYOUT_COMPACT else hdr_view(raw.view(HDR_DTYPE), n, max_headers, layout)
+    hv = None if layout in (LAYOUT_COMPACT, LAYOUT_DENSE) else hdr_view(raw.view(HDR_DTYPE), n, max_headers, layout)
     res = Result(reqs, hv, None, rw)
+    res.raw_reqs = raw_reqs
     res.raw_hdrs = raw   # the compact layout's records are expanded once the parse has run (_host_done)
     res.raw_http = raw_http if mode == MODE_HTTP else None
     return b, res
 
 
 def _host_done(res: Result, n: int, max_headers: int, layout: int) -> Result:
-    if layout == LAYOUT_COMPACT:
+    if layout == LAYOUT_DENSE:
+        res.reqs = expand_reqs(res.raw_reqs, n, layout)
+    if layout in (LAYOUT_COMPACT, LAYOUT_DENSE):
         res.hdrs = expand_records(res.reqs, res.raw_hdrs, n, max_headers, layout)
     if res.raw_http is not None:
         res.http = expand_http(res.reqs, res.raw_http, n, layout)
@@ -433,7 +466,7 @@ class DeviceBatch:
         self.flags = flags
         self.bytes = torch.from_numpy(buf).to(device)
         self.offsets = torch.from_numpy(off.view(np.int64)).to(device)
-        self.reqs = torch.zeros(self.n * REQ_DTYPE.itemsize, dtype=torch.uint8, device=device)
+        self.reqs = torch.zeros(max(reqs_bytes(self.n, layout), 8), dtype=torch.uint8, device=device)
         self.hdrs = torch.zeros(max(hdrs_bytes(self.n, max_headers, layout), 8), dtype=torch.uint8, device=device)
         self.http = torch.zeros(http_bytes(self.n, mode, layout), dtype=torch.uint8, device=device)
         self.work = torch.zeros(RHP_WORK_WORDS, dtype=torch.int32, device=device)
@@ -458,14 +491,16 @@ class DeviceBatch:
     def result(self) -> Result:
         import torch
         torch.cuda.synchronize()
-        reqs = self.reqs.cpu().numpy().view(REQ_DTYPE)
+        raw_reqs = self.reqs.cpu().numpy()
+        reqs = expand_reqs(raw_reqs, self.n, self.layout)
         raw = self.hdrs.cpu().numpy()
-        hdrs = (expand_records(reqs, raw, self.n, self.max_headers, self.layout) if self.layout == LAYOUT_COMPACT
+        hdrs = (expand_records(reqs, raw, self.n, self.max_headers, self.layout)
+                if self.layout in (LAYOUT_COMPACT, LAYOUT_DENSE)
                 else hdr_view(raw.view(HDR_DTYPE), self.n, self.max_headers, self.layout))
         raw_http = self.http.cpu().numpy() if self.mode == MODE_HTTP else None
         http = expand_http(reqs, raw_http, self.n, self.layout) if self.mode == MODE_HTTP else None
         out = self.bytes.cpu().numpy() if self.mode == MODE_HTTP else None
-        return Result(reqs, hdrs, http, out, raw, raw_http)
+        return Result(reqs, hdrs, http, out, raw, raw_http, raw_reqs)
 
 
 def parse_batch(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: int = MODE_PHR,

@@ -14,6 +14,7 @@
  */
 #include <stdint.h>
 #include <string.h>
+#include <algorithm>
 #include <vector>
 
 #include "rhp.h"
@@ -39,10 +40,11 @@ struct Stats {
  * or the wide area behind the lengths of a compact batch (rhp.h) */
 rhp_hdr_t *wide_records(const rhp_batch_t *b, uint32_t i, uint64_t &hs_hdr)
 {
-  if (b->layout == RHP_LAYOUT_COMPACT) {
+  if (b->layout == RHP_LAYOUT_COMPACT || b->layout == RHP_LAYOUT_DENSE) {
     hs_hdr = 1u;
-    return reinterpret_cast<rhp_hdr_t *>(reinterpret_cast<uint8_t *>(b->hdrs) + RHP_COMPACT_WIDE_OFF(b->n, b->max_headers)) +
-           (uint64_t) i * b->max_headers;
+    const size_t off = b->layout == RHP_LAYOUT_DENSE ? RHP_DENSE_WIDE_OFF(b->n, b->max_headers)
+                                                     : RHP_COMPACT_WIDE_OFF(b->n, b->max_headers);
+    return reinterpret_cast<rhp_hdr_t *>(reinterpret_cast<uint8_t *>(b->hdrs) + off) + (uint64_t) i * b->max_headers;
   }
   const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR;
   hs_hdr = hmajor ? b->n : 1u;
@@ -77,10 +79,30 @@ uint64_t compact_consumed(int32_t ret, const rhp_http_t &x)
   return x.result == 1 ? (uint64_t) ret + (x.body_kind == 1 ? x.body_len : 0u) : 0u;
 }
 
+/* the layouts whose records of an exact-path request are the wide ones */
+bool wide_layout(const rhp_batch_t *b) { return b->layout == RHP_LAYOUT_COMPACT || b->layout == RHP_LAYOUT_DENSE; }
+
+/* dense layout (rhp.h RHP_LAYOUT_DENSE): the 8-byte records and their wide area */
+rhp_req_dense_t *dense_reqs(const rhp_batch_t *b) { return reinterpret_cast<rhp_req_dense_t *>(b->reqs); }
+rhp_req_t *dense_wide_reqs(const rhp_batch_t *b)
+{
+  return reinterpret_cast<rhp_req_t *>(reinterpret_cast<uint8_t *>(b->reqs) + RHP_DENSE_REQ_WIDE_OFF(b->n));
+}
+/* request i's record: rhp_req_t, or (dense) the wide area and a WIDE mark */
+void put_req(const rhp_batch_t *b, uint32_t i, const rhp_req_t &r)
+{
+  if (b->layout != RHP_LAYOUT_DENSE) {
+    b->reqs[i] = r;
+    return;
+  }
+  dense_wide_reqs(b)[i] = r;
+  dense_reqs(b)[i] = rhp_req_dense_t{0, 0, 0, 0, 0, (uint8_t) RHP_DENSE_WIDE};
+}
+
 void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
 {
   rhp_req_t r;
-  r.flags = RHP_F_EXACT | (b->layout == RHP_LAYOUT_COMPACT ? RHP_F_WIDE : 0u);
+  r.flags = RHP_F_EXACT | (wide_layout(b) ? RHP_F_WIDE : 0u);
   uint64_t hs_hdr = 1;
   rhp_hdr_t *h = wide_records(b, i, hs_hdr);
   if (b->mode == RHP_MODE_HTTP) {
@@ -96,19 +118,21 @@ void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
       memset(&r, 0, sizeof r);
       r.ret = pre;
       r.minor_version = -1;
-      r.flags = RHP_F_EXACT | (b->layout == RHP_LAYOUT_COMPACT ? RHP_F_WIDE : 0u);
+      r.flags = RHP_F_EXACT | (wide_layout(b) ? RHP_F_WIDE : 0u);
     } else {
       scalar_phr(b->bytes + off, len, b->max_headers, &r, h, hs_hdr);
     }
   }
-  b->reqs[i] = r;
+  put_req(b, i, r);
 }
 
 }  // namespace
 
 extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] or NULL */)
 {
-  if (b->layout == RHP_LAYOUT_COMPACT && (b->flags & RHP_BATCH_SPECULATIVE)) return -22;   /* as rhp_parse_batch */
+  if ((b->layout == RHP_LAYOUT_COMPACT || b->layout == RHP_LAYOUT_DENSE) && (b->flags & RHP_BATCH_SPECULATIVE))
+    return -22;   /* as rhp_parse_batch */
+  if (b->layout == RHP_LAYOUT_DENSE && b->mode != RHP_MODE_PHR) return -22;
   const Table2 &T = table();
   const uint8_t *cls = T.b + kClassRow * 256u;
   Stats st_count = {0, 0, 0};
@@ -128,11 +152,13 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
     uint32_t st = idx2(byte_class_ctlx(b->bytes[off]) ? S_SLOW : S_PRE, 0);
     Dec d;
     dec_reset(d);
-    const bool compact = b->layout == RHP_LAYOUT_COMPACT;
+    const bool compact = b->layout == RHP_LAYOUT_COMPACT, dense = b->layout == RHP_LAYOUT_DENSE;
     const uint64_t hs_req = b->layout == RHP_LAYOUT_HEADER_MAJOR ? 1u : maxh;
     const uint64_t hs_hdr = b->layout == RHP_LAYOUT_HEADER_MAJOR ? b->n : 1u;
-    rhp_hdr_t *hout = compact ? nullptr : b->hdrs + i * hs_req;
+    rhp_hdr_t *hout = compact || dense ? nullptr : b->hdrs + i * hs_req;
     uint32_t *lens = compact ? reinterpret_cast<uint32_t *>(b->hdrs) + i : nullptr;   /* lens[k * n + i] */
+    uint16_t *lens16 = dense ? reinterpret_cast<uint16_t *>(b->hdrs) + i : nullptr;   /* lens16[k * n + i] */
+    uint32_t fit = 0;   /* dense: max over the request's headers of (name_len << 4, value_len), as the kernel */
     /* the kernel's window: http mode walks RHP_HTTP_BLOCK bytes per window */
     const int32_t block = b->mode == RHP_MODE_HTTP ? RHP_HTTP_BLOCK : RHP_BLOCK;
     constexpr int kMaxWords = (RHP_HTTP_BLOCK > RHP_BLOCK ? RHP_HTTP_BLOCK : RHP_BLOCK) / 32;
@@ -173,6 +199,10 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
           if (dec_event(d, (uint32_t) (block_pos + 32 * w) + bit, maxh, lo, hi)) {
             if (compact) {   /* as the kernel: the two lengths (rhp.h RHP_LAYOUT_COMPACT) */
               lens[(uint64_t) (d.nh - 1) * b->n] = (lo >> 16) | (hi & 0xffff0000u);
+            } else if (dense) {   /* name_len | value_len << 6 (rhp.h RHP_LAYOUT_DENSE), stored whether it fits or not */
+              const uint32_t nl = lo >> 16, vl = hi >> 16;
+              lens16[(uint64_t) (d.nh - 1) * b->n] = (uint16_t) (nl | vl << 6);
+              fit = std::max(fit, std::max(nl << 4, vl));
             } else {
               rhp_hdr_t &o = hout[(uint64_t) (d.nh - 1) * hs_hdr];
               o.name_off = (uint16_t) lo;
@@ -195,6 +225,12 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
         ok = ok && (b->last_len[i] < 3u || b->last_len[i] <= term_pos);
         bad = false;
       }
+      if (ok && dense && ((d.rl01 & 0xffffu) > 255u || fit > RHP_DENSE_VALUE_MAX)) {
+        /* as the kernel: a DFA record the dense fields cannot hold takes the exact path (wide) */
+        st_count.exact++;
+        emu_exact(b, i, off, len);
+        break;
+      }
       if (ok) {
         st_count.fast_ok++;
         rhp_req_t r;
@@ -206,7 +242,11 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
         r.minor_version = (int8_t) (d.rl23 >> 16);
         r.num_headers = (uint16_t) d.nh;
         r.flags = 0;
-        b->reqs[i] = r;
+        if (dense)
+          dense_reqs(b)[i] = rhp_req_dense_t{(uint16_t) r.ret, r.path_len, (uint8_t) r.method_len, (uint8_t) r.num_headers,
+                                             (uint8_t) r.minor_version, 0};
+        else
+          b->reqs[i] = r;
         if (b->mode == RHP_MODE_HTTP && compact) {
           /* as the kernel: with compact records a request that is not GET and
            * has three or more framing candidates (names of 14 or 17 bytes), or
@@ -251,7 +291,8 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
         memset(&r, 0, sizeof r);
         r.ret = -1;
         r.minor_version = -1;
-        b->reqs[i] = r;
+        if (dense) dense_reqs(b)[i] = rhp_req_dense_t{0, 0, 0, 0, 0, (uint8_t) RHP_DENSE_BAD};
+        else b->reqs[i] = r;
         if (b->mode == RHP_MODE_HTTP) {
           rhp_http_t x;
           memset(&x, 0, sizeof x);
@@ -312,12 +353,14 @@ extern "C" int rhp_expand_records(const rhp_batch_t *b, const rhp_req_t *reqs, c
 {
   if (!b || !reqs || !out || (b->max_headers && !hdrs)) return -22;
   const uint32_t n = b->n, m = b->max_headers;
-  const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR, compact = b->layout == RHP_LAYOUT_COMPACT;
+  const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR, dense = b->layout == RHP_LAYOUT_DENSE;
+  const bool compact = b->layout == RHP_LAYOUT_COMPACT || dense;
   if (!hmajor && !compact && b->layout != RHP_LAYOUT_REQUEST_MAJOR) return -22;
   const rhp_hdr_t *h = static_cast<const rhp_hdr_t *>(hdrs);
   const uint32_t *lens = static_cast<const uint32_t *>(hdrs);
-  const rhp_hdr_t *wide =
-      reinterpret_cast<const rhp_hdr_t *>(static_cast<const uint8_t *>(hdrs) + RHP_COMPACT_WIDE_OFF(n, m));
+  const uint16_t *lens16 = static_cast<const uint16_t *>(hdrs);
+  const rhp_hdr_t *wide = reinterpret_cast<const rhp_hdr_t *>(
+      static_cast<const uint8_t *>(hdrs) + (dense ? RHP_DENSE_WIDE_OFF(n, m) : RHP_COMPACT_WIDE_OFF(n, m)));
   for (uint32_t i = 0; i < n; i++) {
     rhp_hdr_t *o = out + (uint64_t) i * m;
     memset(o, 0, sizeof(rhp_hdr_t) * m);
@@ -327,7 +370,16 @@ extern "C" int rhp_expand_records(const rhp_batch_t *b, const rhp_req_t *reqs, c
     if (compact && !(r.flags & RHP_F_WIDE)) {
       uint32_t at = (uint32_t) r.path_off + r.path_len + 11u;   /* the first header line (rhp.h) */
       for (uint32_t k = 0; k < nh; k++) {
-        const uint32_t l = lens[(uint64_t) k * n + i], nl = l & 0xffffu, vl = l >> 16;
+        uint32_t nl, vl;
+        if (dense) {
+          const uint32_t l = lens16[(uint64_t) k * n + i];
+          nl = l & 63u;
+          vl = l >> 6;
+        } else {
+          const uint32_t l = lens[(uint64_t) k * n + i];
+          nl = l & 0xffffu;
+          vl = l >> 16;
+        }
         o[k] = rhp_hdr_t{(uint16_t) at, (uint16_t) nl, (uint16_t) (at + nl + 2u), (uint16_t) vl};
         at += nl + vl + 4u;
       }
@@ -335,6 +387,36 @@ extern "C" int rhp_expand_records(const rhp_batch_t *b, const rhp_req_t *reqs, c
       for (uint32_t k = 0; k < nh; k++)
         o[k] = compact ? wide[(uint64_t) i * m + k] : hmajor ? h[(uint64_t) k * n + i] : h[(uint64_t) i * m + k];
     }
+  }
+  return 0;
+}
+
+extern "C" int rhp_expand_reqs(const rhp_batch_t *b, const void *reqs, rhp_req_t *out)
+{
+  if (!b || !reqs || !out) return -22;
+  if (b->layout != RHP_LAYOUT_DENSE) {
+    memcpy(out, reqs, sizeof(rhp_req_t) * b->n);
+    return 0;
+  }
+  const rhp_req_dense_t *d = static_cast<const rhp_req_dense_t *>(reqs);
+  const rhp_req_t *wide = reinterpret_cast<const rhp_req_t *>(static_cast<const uint8_t *>(reqs) + RHP_DENSE_REQ_WIDE_OFF(b->n));
+  for (uint32_t i = 0; i < b->n; i++) {
+    rhp_req_t r;
+    memset(&r, 0, sizeof r);
+    if (d[i].flags & RHP_DENSE_WIDE) {
+      r = wide[i];
+    } else if (d[i].flags & RHP_DENSE_BAD) {
+      r.ret = -1;
+      r.minor_version = -1;
+    } else {
+      r.ret = d[i].ret;
+      r.method_len = d[i].method_len;
+      r.path_off = (uint16_t) (d[i].method_len + 1u);
+      r.path_len = d[i].path_len;
+      r.minor_version = (int8_t) d[i].minor_version;
+      r.num_headers = d[i].num_headers;
+    }
+    out[i] = r;
   }
   return 0;
 }
@@ -382,6 +464,7 @@ extern "C" int rhp_cpu_parse_batch(const rhp_batch_t *b)
   /* as rhp_parse_batch: compact records in both modes (every record wide: the
    * exact path's), not in a speculative batch */
   if (b->layout == RHP_LAYOUT_COMPACT && (b->flags & RHP_BATCH_SPECULATIVE)) return -22;
+  if (b->layout == RHP_LAYOUT_DENSE && (b->mode != RHP_MODE_PHR || (b->flags & RHP_BATCH_SPECULATIVE))) return -22;
   for (uint32_t i = 0; i < b->n; i++) emu_exact(b, i, b->offsets[i], b->offsets[i + 1] - b->offsets[i]);
   return 0;
 }

@@ -73,6 +73,11 @@ struct Params {
    * rhp_http_compact_t); `http` then points at their wide area, which also
    * holds the replay's hints */
   uint2 *hc;
+  /* RHP_LAYOUT_DENSE (phr mode): the 8-byte request records (rhp_req_dense_t)
+   * and the 2-byte header lengths (header-major); `reqs` and `hdrs` then point
+   * at their wide areas */
+  uint2 *dreq;
+  uint16_t *lens16;
 };
 
 /* http records (RHP_MODE_HTTP).  With compact records (p.hc) a record whose
@@ -114,6 +119,7 @@ enum : uint32_t {
   kStageWave = 64 * kBlock,                      /* one window per lane */
   kPark = 0,                                     /* the DONE index: idle lanes step here */
   kDeferExact = 0x8000u,                         /* reqs[i].flags while deferred (kernel-internal) */
+  kDeferDense = 0x80u,                           /* ... rhp_req_dense_t flags (RHP_LAYOUT_DENSE) */
   /* http mode: the replay's instructions, in the body_kind word of the hint
    * finalize leaves in http[i] (ret in the low 16 bits) */
   kHintExact = 0x40000000u,
@@ -422,7 +428,7 @@ struct DevDechunk {
 __device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64_t off, uint64_t len)
 {
   rhp_req_t r;
-  r.flags = RHP_F_EXACT | (p.lens ? RHP_F_WIDE : 0u);   /* compact layout: this request's records are wide */
+  r.flags = RHP_F_EXACT | (p.lens || p.lens16 ? RHP_F_WIDE : 0u);   /* compact / dense: this request's records are wide */
   rhp_hdr_t *h = p.hdrs + (uint64_t) i * p.hs_req;
   if (p.mode == RHP_MODE_HTTP) {
     rhp_http_t x;
@@ -447,6 +453,7 @@ __device__ __forceinline__ void finish_exact(const Params &p, uint32_t i, uint64
     }
   }
   p.reqs[i] = r;
+  if (p.dreq) p.dreq[i] = uint2{0u, RHP_DENSE_WIDE << 24};   /* dense: the record is the wide one */
 }
 
 /* 28 bytes at b (any alignment) as 7 dwords, from three aligned 16-byte loads:
@@ -973,6 +980,11 @@ __device__ __forceinline__ void store_len_lanes(uint64_t mask, uint32_t *dst, ui
 {
   RHP_STORE_LANES("global_store_dword", mask, dst, v, wt);
 }
+/* the same for a dense header record (RHP_LAYOUT_DENSE: name_len | value_len << 6) */
+__device__ __forceinline__ void store_len16_lanes(uint64_t mask, uint16_t *dst, uint32_t v, bool wt)
+{
+  RHP_STORE_LANES("global_store_short", mask, dst, v, wt);
+}
 /* the request record (16 B) for the active lanes */
 __device__ __forceinline__ void store_req(rhp_req_t *dst, u32x4 v, bool wt)
 {
@@ -1010,9 +1022,16 @@ __device__ __forceinline__ void store_http_bad(rhp_http_t *dst)
  * events of the window walked in the previous iteration) -- the same request
  * unless the lane switched between the two windows.
  */
-template <int WAVES, bool LATE, bool HTTP, bool COMPACT>
+/* REC: the records the loop writes: 0 rhp_hdr_t (request- or header-major), 1
+ * compact (u32 lengths; http mode: compact http records too), 2 dense (u16
+ * lengths and 8-byte request records, phr mode) */
+enum : int { kRecWide = 0, kRecCompact = 1, kRecDense = 2 };
+template <int WAVES, bool LATE, bool HTTP, int REC>
 __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel(Params p)
 {
+  constexpr bool COMPACT = REC != kRecWide;   /* lengths, offsets by the running sum */
+  constexpr bool DENSE = REC == kRecDense;
+  static_assert(!(DENSE && HTTP), "dense records: phr mode only");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
@@ -1154,6 +1173,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   int32_t dpos = 0;                    /* position of the decoded window's first byte */
   uint32_t evp[kWEv];                  /* its events */
   uint32_t kn = 0, me = 0, pe = 0, rl = 0, nh = 0, ls = 0, t = 0, pco = 0, ovf = 0;
+  uint32_t fit = 0;                    /* dense: max over the request's records of (name_len << 4, value_len) */
   uint32_t cand = 0, crec_lo = 0, crec_hi = 0;
   /* http framing in the late-issue kernel (http.c:196-218), from the
    * staging buffer while the decoded window is still in it: the request's
@@ -1313,11 +1333,21 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
             com = t ? com : com & (com - 1u);
             eolm &= eolm - 1u;
             const uint32_t nlen = co - ls, vlen = e - co - 3u;
-            if constexpr (COMPACT) {
+            if constexpr (DENSE) {
+              uint16_t *q = p.lens16 + hx;
+              fit = max(fit, max(nlen << 4, vlen));
+              if constexpr (decltype(wt_c)::value)
+                asm volatile("global_store_short %0, %1, off sc1" ::"v"(q), "v"(nlen | vlen << 6) : "memory");
+              else *GLOBAL(uint16_t, q) = (uint16_t) (nlen | vlen << 6);
+            } else if constexpr (COMPACT) {
               uint32_t *q = p.lens + hx;
+#ifdef RHP_DIAG_NO_RECSTORE   /* diagnostic: the records computed, not stored (the stores' share) */
+              asm volatile("" ::"v"(q), "v"(nlen | vlen << 16));
+#else
               if constexpr (decltype(wt_c)::value)
                 asm volatile("global_store_dword %0, %1, off sc1" ::"v"(q), "v"(nlen | vlen << 16) : "memory");
               else *GLOBAL(uint32_t, q) = nlen | vlen << 16;
+#endif
             } else {
               rhp_hdr_t *q = p.hdrs + hx;
               const u32x2 v = u32x2{ls | nlen << 16, (co + 2u) | vlen << 16};
@@ -1349,7 +1379,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         const uint32_t e = base + (uint32_t) __builtin_ctz(eolm | 0x80000000u);
         const uint32_t co = t ? pco : base + (uint32_t) __builtin_ctz(com | 0x80000000u);
         const uint32_t lo = ls | ((co - ls) << 16), hi = (co + 2u) | ((e - co - 3u) << 16);
-        if constexpr (COMPACT) store_len_lanes(st_m, p.lens + hx, (co - ls) | ((e - co - 3u) << 16), wt);
+        if constexpr (DENSE) {
+          store_len16_lanes(st_m, p.lens16 + hx, (co - ls) | ((e - co - 3u) << 6), wt);
+          fit = has ? max(fit, max((co - ls) << 4, e - co - 3u)) : fit;
+        } else if constexpr (COMPACT) store_len_lanes(st_m, p.lens + hx, (co - ls) | ((e - co - 3u) << 16), wt);
         else store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi}, wt);
         if (http) {   /* uniform: framing candidates only in http mode */
           const uint32_t nlen = co - ls;
@@ -1384,9 +1417,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const uint32_t lo = ls | ((co - ls) << 16), hi = (co + 2u) | ((e - co - 3u) << 16);
       const uint64_t st_m = __builtin_amdgcn_ballot_w64(rec);
       if (st_m) {
-        if constexpr (COMPACT) store_len_lanes(st_m, p.lens + hx, (co - ls) | ((e - co - 3u) << 16), wt);
+        if constexpr (DENSE) store_len16_lanes(st_m, p.lens16 + hx, (co - ls) | ((e - co - 3u) << 6), wt);
+        else if constexpr (COMPACT) store_len_lanes(st_m, p.lens + hx, (co - ls) | ((e - co - 3u) << 16), wt);
         else store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi}, wt);
       }
+      if constexpr (DENSE) fit = rec ? max(fit, max((co - ls) << 4, e - co - 3u)) : fit;
       if (http) {
         const uint32_t nlen = co - ls;
         const bool cnd = rec && (nlen == 14u || nlen == 17u);
@@ -1583,6 +1618,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
      * len >= PE + 10 */
     bool bad = ovfl ? ovf - 1u < dlen
                     : (is_err2(e) && term_pos < dlen && ((kn & 7u) != 2u || pe + 10u <= dlen));
+#ifdef RHP_DIAG_NO_WALK
+    ok = false;   /* diagnostic: nothing was walked; every request ends at its last window, -1, no replay */
+    bad = true;
+#endif
     if (!http && p.last_len) {
       /* last_len != 0 (rare: a batch that carries it): is_complete runs first
        * (picohttpparser.c:399-401).  Scanning from last_len - 3 at or before
@@ -1595,6 +1634,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         bad = false;
       }
     }
+    /* dense records (phr mode): a DFA record whose method is longer than 255
+     * bytes or one of whose header records does not fit the 2-byte form takes
+     * the exact path (the wide records) */
+    if constexpr (DENSE) ok = ok && (rl & 0xffffu) <= 255u && fit <= RHP_DENSE_VALUE_MAX;
     /* the record as four dwords (rhp.h rhp_req_t: ret; method_len, path_off;
      * path_len, method_off 0, minor_version; num_headers, flags) */
     u32x4 rq = u32x4{0u, 0u, 0xff000000u, 0u};   /* minor_version -1 */
@@ -1656,7 +1699,18 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         *GLOBAL(u32x4a4, &p.http[dcur]) = u32x4a4{0u, kHintExact, 0u, 0u};
       }
     }
-    store_req(p.reqs + dcur, rq, wt);
+    if constexpr (DENSE) {
+      /* rhp_req_dense_t: ret | path_len << 16; method_len | num_headers << 8 |
+       * minor << 16 | flags << 24 (bad: RHP_DENSE_BAD; exact: wide, deferred) */
+      const uint32_t w1 = ok ? (rl & 0xffu) | (nh << 8) | (((kn >> 3) & 1u) << 16)
+                             : bad ? RHP_DENSE_BAD << 24 : (kDeferDense | RHP_DENSE_WIDE) << 24;
+      const u32x2 v = u32x2{ok ? (term_pos + 1u) | (rl & 0xffff0000u) : 0u, w1};
+      uint2 *q = p.dreq + dcur;
+      if (wt) asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(q), "v"(v) : "memory");
+      else *GLOBAL(u32x2, q) = v;
+    } else {
+      store_req(p.reqs + dcur, rq, wt);
+    }
     dhas = false;
     return true;
   };
@@ -1816,6 +1870,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   const bool uneven =
       may_order && __builtin_amdgcn_ballot_w64((uint64_t) (s1 - s0) * span_n > 2u * (o_hi - o_lo)) != 0;
   wt = p.wt_records && !uneven;
+#ifdef RHP_DIAG_NO_WT   /* diagnostic: plain record stores everywhere */
+  wt = false;
+#endif
   /* An uneven range runs on 15 of the 16 waves (14 when its order needs two
    * waves' staging; the others hold the hand-out order and only join the
    * barriers and the replay).
@@ -1984,14 +2041,27 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       dg.section(1, true);
       /* [F] walk + decode of the previous window */
       decode_begin();
+#ifndef RHP_DIAG_NO_DECODE   /* diagnostic builds only (records not written): the decode's share of the loop */
       if (any_dec) decode_window();
+#endif
 #pragma unroll
       for (int w = 0; w < (int) kWEv; w++) ev[w] = 0;
       dg.section(2, true, true);
       if (any_walk) {
         if (!walking) st = kPark;   /* idle lanes step in the parked terminal state */
         zero_lead(wnew);
+#ifndef RHP_DIAG_NO_WALK   /* diagnostic builds only (every request then ends at its buffer's end): the walk's share */
+#ifdef RHP_DIAG_WALK_TWICE   /* diagnostic: the window walked twice from the same state (same outputs): a walk's marginal cost */
+        {
+          uint32_t st0 = st;
+          opaque(st0);
+          walk();
+          opaque(st);
+          st = st0;
+        }
+#endif
         walk();
+#endif
       }
     } else {
       /* [F] walk, then decode the walked window at once (not one behind): a
@@ -2015,7 +2085,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         dcur = wcur;
         dlen = wlen;
         doff = woff;
-        kn = me = pe = rl = nh = ls = t = pco = ovf = 0;
+        kn = me = pe = rl = nh = ls = t = pco = ovf = fit = 0;
         cand = wget;
         crec_lo = crec_hi = 0;
         fr = 0;
@@ -2057,7 +2127,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         dcur = wcur;
         dlen = wlen;
         if constexpr (LATE) doff = woff;
-        kn = me = pe = rl = nh = ls = t = pco = ovf = 0;
+        kn = me = pe = rl = nh = ls = t = pco = ovf = fit = 0;
         cand = wget;
         crec_lo = crec_hi = 0;
       }
@@ -2121,6 +2191,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         h.off = p.offsets[k];
         h.end = p.offsets[k + 1];
         if (http) h.hint = *GLOBAL(const u32x4a4, &p.http[k]);
+        else if (DENSE) h.f = (p.dreq[k].y >> 24) & kDeferDense ? kDeferExact : 0u;
         else h.f = p.reqs[k].flags;
       }
       return h;
@@ -2366,7 +2437,7 @@ int device_cus(int dev, int *cus)
   return 0;
 }
 
-template <int WAVES, bool LATE, bool HTTP, bool COMPACT>
+template <int WAVES, bool LATE, bool HTTP, int REC>
 int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
 {
   constexpr uint32_t kX = (LATE && HTTP) ? kHttpXParts : 0u;
@@ -2375,10 +2446,10 @@ int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
   constexpr size_t lds_bytes = kLdsTable + (size_t) WAVES * kStageWave + kPoolBytes + 4u * kOrderBuckets +
                                (size_t) WAVES * 1024u * kX;
   static_assert(lds_bytes <= 160u * 1024u, "the workgroup's LDS fits the CU's 160 KiB");
-  const uint64_t bit = 1ull << (8 * (WAVES / 4) + (COMPACT ? 4 : 0) + (LATE ? 2 : 0) + (HTTP ? 1 : 0));
+  const uint64_t bit = 1ull << ((3 * (WAVES / 4) + REC) * 4 + (LATE ? 2 : 0) + (HTTP ? 1 : 0));   /* < 64: WAVES 8/12/16 */
   if (!(g_attr[dev].load(std::memory_order_acquire) & bit)) {
     /* idempotent: two threads of one device may both set it */
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES, LATE, HTTP, COMPACT>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&rhp_dfa_kernel<WAVES, LATE, HTTP, REC>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds_bytes);
     if (e != hipSuccess) return (int) e;
     g_attr[dev].fetch_or(bit, std::memory_order_release);
@@ -2390,7 +2461,7 @@ int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
   /* each workgroup owns a contiguous n/grid share of the requests */
   Params q = prm;
   q.span = (prm.n + grid - 1) / grid;
-  hipLaunchKernelGGL((rhp_dfa_kernel<WAVES, LATE, HTTP, COMPACT>), dim3(grid), dim3(WAVES * 64), lds_bytes, s, q);
+  hipLaunchKernelGGL((rhp_dfa_kernel<WAVES, LATE, HTTP, REC>), dim3(grid), dim3(WAVES * 64), lds_bytes, s, q);
   return (int) hipGetLastError();
 }
 
@@ -2439,7 +2510,8 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   if (b->mode == RHP_MODE_HTTP && (!b->http || !b->bytes_rw)) return -22;
   if (b->mode != RHP_MODE_PHR && b->mode != RHP_MODE_HTTP) return -22;
   if (b->layout != RHP_LAYOUT_REQUEST_MAJOR && b->layout != RHP_LAYOUT_HEADER_MAJOR &&
-      !(b->layout == RHP_LAYOUT_COMPACT && !(b->flags & RHP_BATCH_SPECULATIVE))) return -22;   /* compact: not speculative */
+      !(b->layout == RHP_LAYOUT_COMPACT && !(b->flags & RHP_BATCH_SPECULATIVE)) &&
+      !(b->layout == RHP_LAYOUT_DENSE && b->mode == RHP_MODE_PHR)) return -22;   /* compact: not speculative; dense: phr */
   if (b->last_len && b->mode != RHP_MODE_PHR) return -22;   /* http_read_request passes last_len 0 */
   if ((b->flags & ~RHP_BATCH_SPECULATIVE) || ((b->flags & RHP_BATCH_SPECULATIVE) && b->mode != RHP_MODE_HTTP)) return -22;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -2466,14 +2538,26 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.mode = b->mode;
   prm.span = 0;
   const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR;
-  const bool compact = b->layout == RHP_LAYOUT_COMPACT;
+  const bool compact = b->layout == RHP_LAYOUT_COMPACT, dense = b->layout == RHP_LAYOUT_DENSE;
   prm.hs_req = hmajor ? 1u : b->max_headers;
   prm.hs_hdr = hmajor ? b->n : 1u;
   prm.lens = nullptr;
   prm.hc = nullptr;
+  prm.dreq = nullptr;
+  prm.lens16 = nullptr;
   prm.rec_req = prm.hs_req;
   prm.rec_hdr = prm.hs_hdr;
   prm.wt_records = b->mode == RHP_MODE_PHR && b->layout != RHP_LAYOUT_REQUEST_MAJOR;
+  if (dense) {   /* 8-byte request records and u16 lengths (header-major), the wide ones behind them */
+    prm.dreq = reinterpret_cast<uint2 *>(b->reqs);
+    prm.reqs = reinterpret_cast<rhp_req_t *>(reinterpret_cast<uint8_t *>(b->reqs) + RHP_DENSE_REQ_WIDE_OFF(b->n));
+    prm.lens16 = reinterpret_cast<uint16_t *>(b->hdrs);
+    prm.hdrs = reinterpret_cast<rhp_hdr_t *>(reinterpret_cast<uint8_t *>(b->hdrs) + RHP_DENSE_WIDE_OFF(b->n, b->max_headers));
+    prm.hs_req = b->max_headers;   /* the exact path's wide records: request-major */
+    prm.hs_hdr = 1u;
+    prm.rec_req = 1u;
+    prm.rec_hdr = b->n;
+  }
   if (compact) {   /* lengths header-major at hdrs, the wide records request-major behind them */
     prm.lens = reinterpret_cast<uint32_t *>(b->hdrs);
     prm.hdrs = reinterpret_cast<rhp_hdr_t *>(reinterpret_cast<uint8_t *>(b->hdrs) + RHP_COMPACT_WIDE_OFF(b->n, b->max_headers));
@@ -2495,10 +2579,12 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   }
   const bool late = late_issue(b->mode);
   if (b->mode == RHP_MODE_HTTP)
-    return compact ? launch_dfa<kHttpWaves, true, true, true>(prm, s, dev, cus) : launch_dfa<kHttpWaves, true, true, false>(prm, s, dev, cus);
-  if (compact) return late ? launch_dfa<16, true, false, true>(prm, s, dev, cus) : launch_dfa<16, false, false, true>(prm, s, dev, cus);
-  if (late) return launch_dfa<16, true, false, false>(prm, s, dev, cus);
-  return launch_dfa<16, false, false, false>(prm, s, dev, cus);
+    return compact ? launch_dfa<kHttpWaves, true, true, kRecCompact>(prm, s, dev, cus)
+                   : launch_dfa<kHttpWaves, true, true, kRecWide>(prm, s, dev, cus);
+  if (dense) return late ? launch_dfa<16, true, false, kRecDense>(prm, s, dev, cus) : launch_dfa<16, false, false, kRecDense>(prm, s, dev, cus);
+  if (compact) return late ? launch_dfa<16, true, false, kRecCompact>(prm, s, dev, cus) : launch_dfa<16, false, false, kRecCompact>(prm, s, dev, cus);
+  if (late) return launch_dfa<16, true, false, kRecWide>(prm, s, dev, cus);
+  return launch_dfa<16, false, false, kRecWide>(prm, s, dev, cus);
 }
 
 int rhp_fixup_sessions(const rhp_batch_t *b, const rhp_session_t *sessions, uint32_t n_sessions,

@@ -1,0 +1,165 @@
+"""Dense records (RHP_LAYOUT_DENSE, include/rhp.h; round 6): 8-byte request
+records and 2-byte header lengths for what the DFA parses, the wide rhp_req_t /
+rhp_hdr_t records for everything else.  Expanded (rhp_expand_reqs,
+rhp_expand_records), the records equal the reference's (golden fixtures, the
+oracle, full-size digests) whichever path parsed a request.
+
+CPU: the kernel's emulator and the product's exact parser in the dense layout;
+the fields the dense form cannot hold (a method over 255 bytes, a header name
+of 63+ or a value of 1008+ bytes) send a request to the exact path.
+GPU (-m gpu): the DFA kernel (both loop forms) and the exact kernel in the dense
+layout, against the golden sets, fuzz at every max_headers, the full-size
+digests of configs 2/3/4, edge cases at every alignment, last_len; the
+DFA/exact choice equals the emulator's."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import libreactorng_amd as rhp
+from golden_sets import inputs, record_digest
+from oracle_util import assert_same, canon, run_oracle, to_rhp
+from batches import EDGE, pack
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+SETS = json.load(open(os.path.join(GOLDEN, "manifest.json")))["sets"]
+FULL = json.load(open(os.path.join(GOLDEN, "full_digests.json")))["sets"]
+PHR_SETS = sorted(k for k, v in SETS.items() if v["mode"] == rhp.MODE_PHR)
+D = rhp.LAYOUT_DENSE
+
+
+def golden(name):
+    spec = SETS[name]
+    buf, off = inputs(spec)
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    return spec, buf, off, (z["reqs"], z["hdrs"], None)
+
+
+def dense_fields(res, n):
+    """(flags, ret) of the raw rhp_req_dense_t records"""
+    raw = res.raw_reqs[: 8 * n].reshape(n, 8)
+    return raw[:, 7], raw[:, 0].astype(np.uint32) | raw[:, 1].astype(np.uint32) << 8
+
+
+def long_fields():
+    """requests whose DFA records the dense fields cannot hold, beside ones they can"""
+    return [b"GET / HTTP/1.1\r\nHost: a\r\n\r\n",
+            b"M" * 256 + b" / HTTP/1.1\r\nHost: a\r\n\r\n",                     # method 256 B
+            b"M" * 255 + b" / HTTP/1.1\r\nHost: a\r\n\r\n",                     # method 255 B: dense
+            b"GET / HTTP/1.1\r\n" + b"N" * 63 + b": v\r\n\r\n",                 # name 63 B
+            b"GET / HTTP/1.1\r\n" + b"N" * 62 + b": v\r\n\r\n",                 # name 62 B: dense
+            b"GET / HTTP/1.1\r\nX: " + b"v" * 1008 + b"\r\n\r\n",               # value 1008 B
+            b"GET / HTTP/1.1\r\nX: " + b"v" * 1007 + b"\r\n\r\n",               # value 1007 B: dense
+            b"GET /" + b"p" * 60000 + b" HTTP/1.0\r\nA: b\r\n\r\n",             # long path: dense
+            b"GET / HTTP/1.1\r\nBad Header\r\n\r\n",                            # -1
+            b"GET / HTTP/1.1\r\nA: b\r\n"]                                      # -2: exact
+
+
+@pytest.mark.parametrize("name", PHR_SETS)
+def test_emulation_dense_matches_golden(name):
+    spec, buf, off, want = golden(name)
+    res, _ = rhp.emulate(buf, off, spec["max_headers"], spec["mode"], D)
+    assert_same(canon(res, spec["mode"]), want, buf, off, f"emulation (dense) vs golden {name}")
+    res = rhp.parse_cpu_exact(buf, off, spec["max_headers"], spec["mode"], D)
+    assert_same(canon(res, spec["mode"]), want, buf, off, f"CPU exact (dense) vs golden {name}")
+    flags, _ = dense_fields(res, len(off) - 1)
+    assert (flags & rhp.DENSE_WIDE).all()   # the exact parser's records are all wide
+
+
+def test_dense_field_limits_take_the_exact_path():
+    buf, off = pack(long_fields())
+    want = to_rhp(*run_oracle(buf, off, 16, rhp.MODE_PHR)[:3], rhp.MODE_PHR)
+    res, _ = rhp.emulate(buf, off, 16, rhp.MODE_PHR, D)
+    assert_same(canon(res, rhp.MODE_PHR), want, buf, off, "dense limits (emulation)")
+    flags, _ = dense_fields(res, len(off) - 1)
+    wide = (flags & rhp.DENSE_WIDE) != 0
+    assert list(wide) == [False, True, False, True, False, True, False, False, False, True]
+    assert flags[8] & rhp.DENSE_BAD
+
+
+def test_dense_rejected_outside_phr_mode():
+    buf, off = pack([b"GET / HTTP/1.1\r\n\r\n"])
+    with pytest.raises(RuntimeError):
+        rhp.emulate(buf, off, 16, rhp.MODE_HTTP, D)
+    with pytest.raises(RuntimeError):
+        rhp.parse_cpu_exact(buf, off, 16, rhp.MODE_HTTP, D)
+
+
+def test_dense_sizes():
+    assert rhp.reqs_bytes(1000, D) == 8000 + 16000
+    assert rhp.hdrs_bytes(1000, 16, D) == 32000 + 128000
+    assert rhp.hdrs_bytes(3, 3, D) == 32 + 72   # the wide area 16-byte aligned
+
+
+# ------------------------------------------------------------------ GPU
+
+IMPLS = [rhp.IMPL_DFA, rhp.IMPL_DFA_LATE, rhp.IMPL_EXACT]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("impl", IMPLS)
+@pytest.mark.parametrize("name", PHR_SETS)
+def test_gpu_dense_matches_reference_golden(name, impl):
+    spec, buf, off, want = golden(name)
+    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], impl=impl, layout=D)
+    assert_same(canon(res, spec["mode"]), want, buf, off, f"GPU dense impl{impl} vs golden {name}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("maxh", [0, 1, 3, 16, 32, 64])
+def test_gpu_dense_fuzz_vs_oracle(maxh):
+    for impl, seed in ((rhp.IMPL_DFA, 9600 + maxh), (rhp.IMPL_DFA_LATE, 9700 + maxh)):
+        buf, off = rhp.generate(rhp.GEN_FUZZ, 60000, seed)
+        res = rhp.parse_batch(buf, off, maxh, rhp.MODE_PHR, impl=impl, layout=D)
+        want = to_rhp(*run_oracle(buf, off, maxh, rhp.MODE_PHR)[:3], rhp.MODE_PHR)
+        assert_same(canon(res, rhp.MODE_PHR), want, buf, off, f"GPU dense fuzz impl{impl} maxh{maxh}")
+        emu, _ = rhp.emulate(buf, off, maxh, rhp.MODE_PHR, D)
+        assert np.array_equal(res.reqs["flags"] & (rhp.F_EXACT | rhp.F_WIDE), emu.reqs["flags"] & (rhp.F_EXACT | rhp.F_WIDE))
+
+
+@pytest.mark.gpu
+def test_gpu_dense_field_limits():
+    buf, off = pack(long_fields() * 40)
+    want = to_rhp(*run_oracle(buf, off, 16, rhp.MODE_PHR)[:3], rhp.MODE_PHR)
+    for impl in IMPLS:
+        res = rhp.parse_batch(buf, off, 16, rhp.MODE_PHR, impl=impl, layout=D)
+        assert_same(canon(res, rhp.MODE_PHR), want, buf, off, f"GPU dense limits impl{impl}")
+    emu, _ = rhp.emulate(buf, off, 16, rhp.MODE_PHR, D)
+    res = rhp.parse_batch(buf, off, 16, rhp.MODE_PHR, layout=D)
+    assert np.array_equal(dense_fields(res, len(off) - 1)[0], dense_fields(emu, len(off) - 1)[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["config2_get256_h16", "config3_zipf_h32", "config4_get256_shard5of8",
+                                  "config4_get256_shard7of8"])
+def test_gpu_dense_full_size_matches_reference_digest(name):
+    spec = FULL[name]
+    buf, off = inputs(spec)
+    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], layout=D)
+    got = canon(res, spec["mode"])
+    if record_digest(*got) != spec["records_sha256"]:
+        want = to_rhp(*run_oracle(buf, off, spec["max_headers"], spec["mode"])[:3], spec["mode"])
+        assert_same(got, want, buf, off, name)
+        raise AssertionError(f"{name}: dense digest differs from the reference but matches the oracle")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+def test_gpu_dense_edge_cases(shift):
+    buf, off = pack(EDGE * 3, align_shift=shift)
+    for maxh in (0, 1, 16):
+        want = to_rhp(*run_oracle(buf, off, maxh, rhp.MODE_PHR)[:3], rhp.MODE_PHR)
+        res = rhp.parse_batch(buf, off, maxh, rhp.MODE_PHR, layout=D)
+        assert_same(canon(res, rhp.MODE_PHR), want, buf, off, f"GPU dense edge shift{shift} maxh{maxh}")
+
+
+@pytest.mark.gpu
+def test_gpu_dense_last_len_matches_reference_golden():
+    top = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    buf, off = inputs(top["phr_last_len"])
+    z = np.load(os.path.join(GOLDEN, "phr_last_len.npz"))
+    for impl in IMPLS:
+        res = rhp.parse_batch(buf, off, 16, rhp.MODE_PHR, impl=impl, layout=D, last_len=z["last_len"])
+        assert_same(canon(res, rhp.MODE_PHR), (z["reqs"], z["hdrs"], None), buf, off, f"GPU dense impl{impl} last_len")

@@ -3,7 +3,12 @@
 # bench line, rocprofv3 kernel-trace summaries of configs 2/3/5 and PMC
 # FETCH_SIZE / WRITE_SIZE passes (separate runs).  Every GPU step has its own
 # time limit; steps are chained with && so a failure stops the session.
-# STEPS=tests,bench,prof,pmc,sq,writer,smoke,ceil (default all but ceil)
+# STEPS=tests,bench,prof,pmc,sq,writer,smoke,ceil (default all but ceil); also
+#   quick  the GPU tests whose names match TESTS_K (pytest -k)
+#   lines  tools/ubench_lines (window line order vs bandwidth; built beforehand)
+#   ab     tools/ab_libs.py over AB_LIBS ("tag=path ...") for each of AB_CONFIGS
+# (round 6: one script for every session; the per-session env is recorded in
+# the profiles README that keeps its output)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out && export TMPDIR=/tmp
 TAG=${TAG:-s}
@@ -51,10 +56,25 @@ step_ceil() {
   # the read + record-write ceiling microbenchmark (built on the CPU beforehand), its ONLY_C forms
   ONLY_C=1 timeout -k 10 180 tools/ubench_ceiling > gpurun_out/ceil_${TAG}.txt 2>&1 && cat gpurun_out/ceil_${TAG}.txt
 }
+step_quick() {
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${TESTS_K}" \
+    > gpurun_out/pytest_${TAG}.log 2>&1 && echo QUICK_OK && tail -3 gpurun_out/pytest_${TAG}.log
+}
+step_lines() {
+  timeout -k 10 180 tools/ubench_lines > gpurun_out/lines_${TAG}.txt 2>&1 && cat gpurun_out/lines_${TAG}.txt
+}
+step_ab() {
+  for c in ${AB_CONFIGS:-get256}; do
+    timeout -k 10 ${AB_TIMEOUT:-300} python3 -u tools/ab_libs.py --config $c --rounds ${AB_ROUNDS:-7} --steps ${AB_STEPS:-30} \
+      ${AB_ARGS} ${AB_LIBS} > gpurun_out/ab_${TAG}_$c.txt 2>&1 || { tail -5 gpurun_out/ab_${TAG}_$c.txt; return 1; }
+    grep "^ab $c\|parity" gpurun_out/ab_${TAG}_$c.txt
+  done
+}
 step_smoke() {
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" > gpurun_out/smoke_${TAG}.log 2>&1 \
     && tail -1 gpurun_out/smoke_${TAG}.log
 }
-( ! has tests || step_tests ) && ( ! has bench || step_bench ) && ( ! has prof || step_prof ) && ( ! has pmc || step_pmc ) \
+( ! has quick || step_quick ) && ( ! has lines || step_lines ) && ( ! has ab || step_ab ) \
+  && ( ! has tests || step_tests ) && ( ! has bench || step_bench ) && ( ! has prof || step_prof ) && ( ! has pmc || step_pmc ) \
   && ( ! has sq || step_sq ) && ( ! has writer || step_writer ) && ( ! has smoke || step_smoke ) \
   && ( ! has ceil || step_ceil ) && echo SESSION_OK

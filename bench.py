@@ -51,7 +51,7 @@ sys.path.insert(0, ROOT)
 import libreactorng_amd as rhp  # noqa: E402
 
 LAYOUTS = {"request": rhp.LAYOUT_REQUEST_MAJOR, "header": rhp.LAYOUT_HEADER_MAJOR, "compact": rhp.LAYOUT_COMPACT,
-           "dense": rhp.LAYOUT_DENSE}
+           "dense": rhp.LAYOUT_DENSE, "dense_rm": rhp.LAYOUT_DENSE_RM}
 METRIC = "GiB/s device-resident batched HTTP/1.1 request parse, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E, GB/s (MI355X_MICROARCH.md chip table)
 CONFIGS = {
@@ -59,7 +59,7 @@ CONFIGS = {
                    layout="dense",
                    name="config2/4: 1M x 256 B GET, 4 headers per GPU (phr_parse_request, max_headers 16)"),
     "zipf": dict(gen=rhp.GEN_ZIPF, seed=0x5EED0003, maxh=32, mode=rhp.MODE_PHR, per_gpu=1 << 20,
-                 layout="request",
+                 layout="dense_rm",
                  name="config3: 1M mixed 64 B-4 KiB Zipf requests, 0-32 headers (max_headers 32)"),
     "post": dict(gen=rhp.GEN_POST1K, seed=0x5EED0005, maxh=16, mode=rhp.MODE_HTTP, per_gpu=1 << 20,
                  layout="compact",
@@ -541,8 +541,8 @@ def main(argv=None):
     ap.add_argument("--layout", default="auto", choices=["auto"] + sorted(LAYOUTS),
                     help="header record layout of the batch ABI (include/rhp.h rhp_layout); auto: the "
                          "config's (dense 8-byte request / 2-byte header records for the uniform phr batches of "
-                         "configs 2/4, compact records for config 5 (http mode), header-major for the chunked "
-                         "config, request-major for config 3's mixed one)")
+                         "configs 2/4 (header-major) and config 3 (request-major: its header counts vary), compact "
+                         "records for config 5 (http mode), header-major for the chunked config)")
     argv = sys.argv[1:] if argv is None else argv
     args = ap.parse_args(argv)
 

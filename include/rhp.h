@@ -83,7 +83,8 @@ enum rhp_layout {
   RHP_LAYOUT_HEADER_MAJOR = 1,
   RHP_LAYOUT_COMPACT = 2,     /* 4-byte header records, below (http mode: 8-byte http records too;
                                  not with RHP_BATCH_SPECULATIVE) */
-  RHP_LAYOUT_DENSE = 3        /* RHP_MODE_PHR: 8-byte request and 2-byte header records, below */
+  RHP_LAYOUT_DENSE = 3,       /* RHP_MODE_PHR: 8-byte request and 2-byte header records, below */
+  RHP_LAYOUT_DENSE_RM = 4     /* the same, the header records request-major */
 };
 /* Compact records (RHP_LAYOUT_COMPACT).  A header line the DFA
  * parses is `name ": " value CRLF` and the first one starts right after the
@@ -102,17 +103,21 @@ enum rhp_layout {
  * 2: 48 -> 32 B per request with the 16-B request record). */
 #define RHP_COMPACT_WIDE_OFF(n, m) ((((size_t) (n) * (size_t) (m) * 4u) + 15u) & ~(size_t) 15u)
 #define RHP_COMPACT_HDRS_BYTES(n, m) (RHP_COMPACT_WIDE_OFF(n, m) + (size_t) (n) * (size_t) (m) * 8u)
-/* Dense records (RHP_LAYOUT_DENSE, RHP_MODE_PHR; round 6).  The compact
- * layout's running-sum offsets with narrower fields, for the DFA's records.
- * reqs holds rhp_req_dense_t dreq[n] (8 B) and, at byte
+/* Dense records (RHP_LAYOUT_DENSE / RHP_LAYOUT_DENSE_RM, RHP_MODE_PHR; round
+ * 6).  The compact layout's running-sum offsets with narrower fields, for the
+ * DFA's records.  reqs holds rhp_req_dense_t dreq[n] (8 B) and, at byte
  * RHP_DENSE_REQ_WIDE_OFF(n), a wide area rhp_req_t wide[n]
- * (RHP_DENSE_REQS_BYTES(n) bytes in all); hdrs holds u16 lens[max_headers][n]
- * (header-major), name_len | value_len << 6, and at byte RHP_DENSE_WIDE_OFF(n, m)
- * the wide header records rhp_hdr_t wide[n][m] (RHP_DENSE_HDRS_BYTES(n, m)).
- * A DFA record is dense when it fits: method_len <= 255 (path_off = method_len
- * + 1, method_off = 0), every header name < 63 and value < 1008 bytes; any other
- * request (those, and every request the exact path parses) is wide: dreq[i].flags
- * holds RHP_DENSE_WIDE and its records are wide[i] and the wide header records.
+ * (RHP_DENSE_REQS_BYTES(n) bytes in all).  hdrs holds u16 lens, name_len |
+ * value_len << 6, at index k * n + i (RHP_LAYOUT_DENSE, header-major) or
+ * i * m + k (RHP_LAYOUT_DENSE_RM, request-major); a header whose name is longer
+ * than RHP_DENSE_NAME_MAX or value longer than RHP_DENSE_VALUE_MAX has
+ * RHP_DENSE_OVERFLOW there and its u32 lengths, name_len | value_len << 16, at
+ * the same index of the overflow area at byte RHP_DENSE_OVF_OFF(n, m); the wide
+ * header records rhp_hdr_t wide[n][m] follow at RHP_DENSE_WIDE_OFF(n, m)
+ * (RHP_DENSE_HDRS_BYTES(n, m) bytes in all).  A DFA request is dense when its
+ * method is at most 255 bytes (path_off = method_len + 1, method_off = 0); any
+ * other (and every request the exact path parses) is wide: dreq[i].flags holds
+ * RHP_DENSE_WIDE, its records are wide[i] and the wide header records.
  * RHP_DENSE_BAD: ret = -1 (the other outputs unspecified, as in rhp_req_t).
  * Config 2 writes 8 + 4 x 2 = 16 B of records per request (compact: 32 B).
  * rhp_expand_reqs / rhp_expand_records (rhp_host.h) expand them on the host. */
@@ -130,7 +135,9 @@ typedef struct rhp_req_dense {
 #define RHP_DENSE_VALUE_MAX 1007u /* longest value */
 #define RHP_DENSE_REQ_WIDE_OFF(n) ((((size_t) (n) * 8u) + 15u) & ~(size_t) 15u)
 #define RHP_DENSE_REQS_BYTES(n) (RHP_DENSE_REQ_WIDE_OFF(n) + (size_t) (n) * 16u)
-#define RHP_DENSE_WIDE_OFF(n, m) ((((size_t) (n) * (size_t) (m) * 2u) + 15u) & ~(size_t) 15u)
+#define RHP_DENSE_OVERFLOW 0xFFFFu
+#define RHP_DENSE_OVF_OFF(n, m) ((((size_t) (n) * (size_t) (m) * 2u) + 15u) & ~(size_t) 15u)
+#define RHP_DENSE_WIDE_OFF(n, m) (RHP_DENSE_OVF_OFF(n, m) + ((((size_t) (n) * (size_t) (m) * 4u) + 15u) & ~(size_t) 15u))
 #define RHP_DENSE_HDRS_BYTES(n, m) (RHP_DENSE_WIDE_OFF(n, m) + (size_t) (n) * (size_t) (m) * 8u)
 
 /* record k of request i in a batch of n requests with capacity m */

@@ -27,7 +27,9 @@ RHP_MAX_HEADERS = 64
 RHP_RET_TOOLONG = -3
 RHP_WORK_WORDS = 64
 MODE_PHR, MODE_HTTP = 0, 1
-LAYOUT_REQUEST_MAJOR, LAYOUT_HEADER_MAJOR, LAYOUT_COMPACT, LAYOUT_DENSE = 0, 1, 2, 3
+LAYOUT_REQUEST_MAJOR, LAYOUT_HEADER_MAJOR, LAYOUT_COMPACT, LAYOUT_DENSE, LAYOUT_DENSE_RM = 0, 1, 2, 3, 4
+DENSE_LAYOUTS = (LAYOUT_DENSE, LAYOUT_DENSE_RM)            # rhp.h: 8-byte request records, u16 lengths
+LENGTH_LAYOUTS = (LAYOUT_COMPACT,) + DENSE_LAYOUTS          # records expanded by the running sum
 IMPL_DFA, IMPL_EXACT, IMPL_DFA_LATE = 0, 1, 2
 RHP_NAME_NULL = 0xFFFF
 F_EXACT = 0x1
@@ -322,14 +324,14 @@ def hdrs_bytes(n: int, max_headers: int, layout: int) -> int:
     """bytes the batch's hdrs buffer needs (rhp.h; RHP_COMPACT_HDRS_BYTES / RHP_DENSE_HDRS_BYTES)"""
     if layout == LAYOUT_COMPACT:
         return ((n * max_headers * 4 + 15) & ~15) + n * max_headers * HDR_DTYPE.itemsize
-    if layout == LAYOUT_DENSE:
-        return ((n * max_headers * 2 + 15) & ~15) + n * max_headers * HDR_DTYPE.itemsize
+    if layout in DENSE_LAYOUTS:   # u16 lengths, the u32 overflow area, the wide records
+        return ((n * max_headers * 2 + 15) & ~15) + ((n * max_headers * 4 + 15) & ~15) + n * max_headers * HDR_DTYPE.itemsize
     return n * max_headers * HDR_DTYPE.itemsize
 
 
 def reqs_bytes(n: int, layout: int) -> int:
     """bytes the batch's reqs buffer needs (rhp.h; RHP_DENSE_REQS_BYTES for the dense layout)"""
-    if layout == LAYOUT_DENSE:
+    if layout in DENSE_LAYOUTS:
         return ((n * 8 + 15) & ~15) + n * REQ_DTYPE.itemsize
     return n * REQ_DTYPE.itemsize
 
@@ -338,7 +340,7 @@ def expand_reqs(raw: np.ndarray, n: int, layout: int) -> np.ndarray:
     """[n] rhp_req_t records of a parsed batch from its raw reqs bytes in any layout
     (rhp_expand_reqs, include/rhp_host.h: dense records expanded)."""
     raw = np.ascontiguousarray(raw).view(np.uint8)
-    if layout != LAYOUT_DENSE:
+    if layout not in DENSE_LAYOUTS:
         return raw[: n * REQ_DTYPE.itemsize].view(REQ_DTYPE).copy()
     out = np.zeros(n, dtype=REQ_DTYPE)
     if n == 0:
@@ -408,7 +410,7 @@ def _host_batch(buf, off, max_headers, mode, layout=LAYOUT_REQUEST_MAJOR, last_l
     rw = buf.copy()
     b = Batch(_ptr(rw), _ptr(rw), _ptr(off), rw.size, n, max_headers, mode, layout, _ptr(raw_reqs), _ptr(raw),
               _ptr(raw_http), 0, flags, 0, _ptr(last_len) if last_len is not None else None)
-    hv = None if layout in (LAYOUT_COMPACT, LAYOUT_DENSE) else hdr_view(raw.view(HDR_DTYPE), n, max_headers, layout)
+    hv = None if layout in LENGTH_LAYOUTS else hdr_view(raw.view(HDR_DTYPE), n, max_headers, layout)
     res = Result(reqs, hv, None, rw)
     res.raw_reqs = raw_reqs
     res.raw_hdrs = raw   # the compact layout's records are expanded once the parse has run (_host_done)
@@ -417,9 +419,9 @@ def _host_batch(buf, off, max_headers, mode, layout=LAYOUT_REQUEST_MAJOR, last_l
 
 
 def _host_done(res: Result, n: int, max_headers: int, layout: int) -> Result:
-    if layout == LAYOUT_DENSE:
+    if layout in DENSE_LAYOUTS:
         res.reqs = expand_reqs(res.raw_reqs, n, layout)
-    if layout in (LAYOUT_COMPACT, LAYOUT_DENSE):
+    if layout in LENGTH_LAYOUTS:
         res.hdrs = expand_records(res.reqs, res.raw_hdrs, n, max_headers, layout)
     if res.raw_http is not None:
         res.http = expand_http(res.reqs, res.raw_http, n, layout)
@@ -495,7 +497,7 @@ class DeviceBatch:
         reqs = expand_reqs(raw_reqs, self.n, self.layout)
         raw = self.hdrs.cpu().numpy()
         hdrs = (expand_records(reqs, raw, self.n, self.max_headers, self.layout)
-                if self.layout in (LAYOUT_COMPACT, LAYOUT_DENSE)
+                if self.layout in LENGTH_LAYOUTS
                 else hdr_view(raw.view(HDR_DTYPE), self.n, self.max_headers, self.layout))
         raw_http = self.http.cpu().numpy() if self.mode == MODE_HTTP else None
         http = expand_http(reqs, raw_http, self.n, self.layout) if self.mode == MODE_HTTP else None

@@ -40,10 +40,10 @@ struct Stats {
  * or the wide area behind the lengths of a compact batch (rhp.h) */
 rhp_hdr_t *wide_records(const rhp_batch_t *b, uint32_t i, uint64_t &hs_hdr)
 {
-  if (b->layout == RHP_LAYOUT_COMPACT || b->layout == RHP_LAYOUT_DENSE) {
+  if (b->layout == RHP_LAYOUT_COMPACT || b->layout == RHP_LAYOUT_DENSE || b->layout == RHP_LAYOUT_DENSE_RM) {
     hs_hdr = 1u;
-    const size_t off = b->layout == RHP_LAYOUT_DENSE ? RHP_DENSE_WIDE_OFF(b->n, b->max_headers)
-                                                     : RHP_COMPACT_WIDE_OFF(b->n, b->max_headers);
+    const size_t off = b->layout != RHP_LAYOUT_COMPACT ? RHP_DENSE_WIDE_OFF(b->n, b->max_headers)
+                                                       : RHP_COMPACT_WIDE_OFF(b->n, b->max_headers);
     return reinterpret_cast<rhp_hdr_t *>(reinterpret_cast<uint8_t *>(b->hdrs) + off) + (uint64_t) i * b->max_headers;
   }
   const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR;
@@ -80,7 +80,8 @@ uint64_t compact_consumed(int32_t ret, const rhp_http_t &x)
 }
 
 /* the layouts whose records of an exact-path request are the wide ones */
-bool wide_layout(const rhp_batch_t *b) { return b->layout == RHP_LAYOUT_COMPACT || b->layout == RHP_LAYOUT_DENSE; }
+bool dense_layout(const rhp_batch_t *b) { return b->layout == RHP_LAYOUT_DENSE || b->layout == RHP_LAYOUT_DENSE_RM; }
+bool wide_layout(const rhp_batch_t *b) { return b->layout == RHP_LAYOUT_COMPACT || dense_layout(b); }
 
 /* dense layout (rhp.h RHP_LAYOUT_DENSE): the 8-byte records and their wide area */
 rhp_req_dense_t *dense_reqs(const rhp_batch_t *b) { return reinterpret_cast<rhp_req_dense_t *>(b->reqs); }
@@ -91,7 +92,7 @@ rhp_req_t *dense_wide_reqs(const rhp_batch_t *b)
 /* request i's record: rhp_req_t, or (dense) the wide area and a WIDE mark */
 void put_req(const rhp_batch_t *b, uint32_t i, const rhp_req_t &r)
 {
-  if (b->layout != RHP_LAYOUT_DENSE) {
+  if (!dense_layout(b)) {
     b->reqs[i] = r;
     return;
   }
@@ -130,9 +131,9 @@ void emu_exact(const rhp_batch_t *b, uint32_t i, uint64_t off, uint64_t len)
 
 extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] or NULL */)
 {
-  if ((b->layout == RHP_LAYOUT_COMPACT || b->layout == RHP_LAYOUT_DENSE) && (b->flags & RHP_BATCH_SPECULATIVE))
+  if ((b->layout == RHP_LAYOUT_COMPACT || dense_layout(b)) && (b->flags & RHP_BATCH_SPECULATIVE))
     return -22;   /* as rhp_parse_batch */
-  if (b->layout == RHP_LAYOUT_DENSE && b->mode != RHP_MODE_PHR) return -22;
+  if (dense_layout(b) && b->mode != RHP_MODE_PHR) return -22;
   const Table2 &T = table();
   const uint8_t *cls = T.b + kClassRow * 256u;
   Stats st_count = {0, 0, 0};
@@ -152,13 +153,18 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
     uint32_t st = idx2(byte_class_ctlx(b->bytes[off]) ? S_SLOW : S_PRE, 0);
     Dec d;
     dec_reset(d);
-    const bool compact = b->layout == RHP_LAYOUT_COMPACT, dense = b->layout == RHP_LAYOUT_DENSE;
+    const bool compact = b->layout == RHP_LAYOUT_COMPACT, dense = dense_layout(b);
     const uint64_t hs_req = b->layout == RHP_LAYOUT_HEADER_MAJOR ? 1u : maxh;
     const uint64_t hs_hdr = b->layout == RHP_LAYOUT_HEADER_MAJOR ? b->n : 1u;
     rhp_hdr_t *hout = compact || dense ? nullptr : b->hdrs + i * hs_req;
     uint32_t *lens = compact ? reinterpret_cast<uint32_t *>(b->hdrs) + i : nullptr;   /* lens[k * n + i] */
-    uint16_t *lens16 = dense ? reinterpret_cast<uint16_t *>(b->hdrs) + i : nullptr;   /* lens16[k * n + i] */
-    uint32_t fit = 0;   /* dense: max over the request's headers of (name_len << 4, value_len), as the kernel */
+    /* dense: the u16 lengths (k * n + i, or request-major i * m + k) and the overflow area */
+    const bool drm = b->layout == RHP_LAYOUT_DENSE_RM;
+    uint16_t *lens16 = dense ? reinterpret_cast<uint16_t *>(b->hdrs) + (drm ? (uint64_t) i * maxh : i) : nullptr;
+    uint32_t *ovf32 = dense ? reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(b->hdrs) + RHP_DENSE_OVF_OFF(b->n, maxh)) +
+                                  (drm ? (uint64_t) i * maxh : i)
+                            : nullptr;
+    const uint64_t dstride = drm ? 1u : b->n;
     /* the kernel's window: http mode walks RHP_HTTP_BLOCK bytes per window */
     const int32_t block = b->mode == RHP_MODE_HTTP ? RHP_HTTP_BLOCK : RHP_BLOCK;
     constexpr int kMaxWords = (RHP_HTTP_BLOCK > RHP_BLOCK ? RHP_HTTP_BLOCK : RHP_BLOCK) / 32;
@@ -199,10 +205,11 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
           if (dec_event(d, (uint32_t) (block_pos + 32 * w) + bit, maxh, lo, hi)) {
             if (compact) {   /* as the kernel: the two lengths (rhp.h RHP_LAYOUT_COMPACT) */
               lens[(uint64_t) (d.nh - 1) * b->n] = (lo >> 16) | (hi & 0xffff0000u);
-            } else if (dense) {   /* name_len | value_len << 6 (rhp.h RHP_LAYOUT_DENSE), stored whether it fits or not */
-              const uint32_t nl = lo >> 16, vl = hi >> 16;
-              lens16[(uint64_t) (d.nh - 1) * b->n] = (uint16_t) (nl | vl << 6);
-              fit = std::max(fit, std::max(nl << 4, vl));
+            } else if (dense) {   /* name_len | value_len << 6 (rhp.h RHP_LAYOUT_DENSE), or the overflow area */
+              const uint32_t nl = lo >> 16, vl = hi >> 16, at = (d.nh - 1) * dstride;
+              const bool fits = std::max(nl << 4, vl) <= RHP_DENSE_VALUE_MAX;
+              lens16[at] = (uint16_t) (fits ? nl | vl << 6 : RHP_DENSE_OVERFLOW);
+              if (!fits) ovf32[at] = nl | vl << 16;
             } else {
               rhp_hdr_t &o = hout[(uint64_t) (d.nh - 1) * hs_hdr];
               o.name_off = (uint16_t) lo;
@@ -225,8 +232,8 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
         ok = ok && (b->last_len[i] < 3u || b->last_len[i] <= term_pos);
         bad = false;
       }
-      if (ok && dense && ((d.rl01 & 0xffffu) > 255u || fit > RHP_DENSE_VALUE_MAX)) {
-        /* as the kernel: a DFA record the dense fields cannot hold takes the exact path (wide) */
+      if (ok && dense && (d.rl01 & 0xffffu) > 255u) {
+        /* as the kernel: a method longer than the dense record holds takes the exact path (wide) */
         st_count.exact++;
         emu_exact(b, i, off, len);
         break;
@@ -353,12 +360,13 @@ extern "C" int rhp_expand_records(const rhp_batch_t *b, const rhp_req_t *reqs, c
 {
   if (!b || !reqs || !out || (b->max_headers && !hdrs)) return -22;
   const uint32_t n = b->n, m = b->max_headers;
-  const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR, dense = b->layout == RHP_LAYOUT_DENSE;
-  const bool compact = b->layout == RHP_LAYOUT_COMPACT || dense;
+  const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR, dense = dense_layout(b);
+  const bool compact = b->layout == RHP_LAYOUT_COMPACT || dense, drm = b->layout == RHP_LAYOUT_DENSE_RM;
   if (!hmajor && !compact && b->layout != RHP_LAYOUT_REQUEST_MAJOR) return -22;
   const rhp_hdr_t *h = static_cast<const rhp_hdr_t *>(hdrs);
   const uint32_t *lens = static_cast<const uint32_t *>(hdrs);
   const uint16_t *lens16 = static_cast<const uint16_t *>(hdrs);
+  const uint32_t *ovf32 = reinterpret_cast<const uint32_t *>(static_cast<const uint8_t *>(hdrs) + RHP_DENSE_OVF_OFF(n, m));
   const rhp_hdr_t *wide = reinterpret_cast<const rhp_hdr_t *>(
       static_cast<const uint8_t *>(hdrs) + (dense ? RHP_DENSE_WIDE_OFF(n, m) : RHP_COMPACT_WIDE_OFF(n, m)));
   for (uint32_t i = 0; i < n; i++) {
@@ -372,9 +380,10 @@ extern "C" int rhp_expand_records(const rhp_batch_t *b, const rhp_req_t *reqs, c
       for (uint32_t k = 0; k < nh; k++) {
         uint32_t nl, vl;
         if (dense) {
-          const uint32_t l = lens16[(uint64_t) k * n + i];
-          nl = l & 63u;
-          vl = l >> 6;
+          const uint64_t at = drm ? (uint64_t) i * m + k : (uint64_t) k * n + i;
+          const uint32_t l = lens16[at], o = l == RHP_DENSE_OVERFLOW ? ovf32[at] : (l & 63u) | (l >> 6) << 16;
+          nl = o & 0xffffu;
+          vl = o >> 16;
         } else {
           const uint32_t l = lens[(uint64_t) k * n + i];
           nl = l & 0xffffu;
@@ -394,7 +403,7 @@ extern "C" int rhp_expand_records(const rhp_batch_t *b, const rhp_req_t *reqs, c
 extern "C" int rhp_expand_reqs(const rhp_batch_t *b, const void *reqs, rhp_req_t *out)
 {
   if (!b || !reqs || !out) return -22;
-  if (b->layout != RHP_LAYOUT_DENSE) {
+  if (!dense_layout(b)) {
     memcpy(out, reqs, sizeof(rhp_req_t) * b->n);
     return 0;
   }
@@ -464,7 +473,7 @@ extern "C" int rhp_cpu_parse_batch(const rhp_batch_t *b)
   /* as rhp_parse_batch: compact records in both modes (every record wide: the
    * exact path's), not in a speculative batch */
   if (b->layout == RHP_LAYOUT_COMPACT && (b->flags & RHP_BATCH_SPECULATIVE)) return -22;
-  if (b->layout == RHP_LAYOUT_DENSE && (b->mode != RHP_MODE_PHR || (b->flags & RHP_BATCH_SPECULATIVE))) return -22;
+  if (dense_layout(b) && (b->mode != RHP_MODE_PHR || (b->flags & RHP_BATCH_SPECULATIVE))) return -22;
   for (uint32_t i = 0; i < b->n; i++) emu_exact(b, i, b->offsets[i], b->offsets[i + 1] - b->offsets[i]);
   return 0;
 }

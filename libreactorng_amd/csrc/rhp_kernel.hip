@@ -78,6 +78,7 @@ struct Params {
    * at their wide areas */
   uint2 *dreq;
   uint16_t *lens16;
+  uint32_t *ovf32;   /* ... and the u32 lengths of the headers the u16 cannot hold */
 };
 
 /* http records (RHP_MODE_HTTP).  With compact records (p.hc) a record whose
@@ -985,6 +986,17 @@ __device__ __forceinline__ void store_len16_lanes(uint64_t mask, uint16_t *dst, 
 {
   RHP_STORE_LANES("global_store_short", mask, dst, v, wt);
 }
+/* a dense header record (RHP_LAYOUT_DENSE: name_len | value_len << 6) for the
+ * lanes in `mask`; one whose lengths do not fit stores RHP_DENSE_OVERFLOW and
+ * its u32 lengths in the overflow area (rare: the lanes that need it, after a
+ * ballot) */
+__device__ __forceinline__ void store_dense_lanes(uint64_t mask, const Params &p, uint32_t hx, uint32_t nlen, uint32_t vlen, bool wt)
+{
+  const bool fits = max(nlen << 4, vlen) <= RHP_DENSE_VALUE_MAX;
+  store_len16_lanes(mask, p.lens16 + hx, fits ? nlen | vlen << 6 : RHP_DENSE_OVERFLOW, wt);
+  const uint64_t over = mask & __builtin_amdgcn_ballot_w64(!fits);
+  if (over) store_len_lanes(over, p.ovf32 + hx, nlen | vlen << 16, false);
+}
 /* the request record (16 B) for the active lanes */
 __device__ __forceinline__ void store_req(rhp_req_t *dst, u32x4 v, bool wt)
 {
@@ -1173,7 +1185,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   int32_t dpos = 0;                    /* position of the decoded window's first byte */
   uint32_t evp[kWEv];                  /* its events */
   uint32_t kn = 0, me = 0, pe = 0, rl = 0, nh = 0, ls = 0, t = 0, pco = 0, ovf = 0;
-  uint32_t fit = 0;                    /* dense: max over the request's records of (name_len << 4, value_len) */
   uint32_t cand = 0, crec_lo = 0, crec_hi = 0;
   /* http framing in the late-issue kernel (http.c:196-218), from the
    * staging buffer while the decoded window is still in it: the request's
@@ -1335,10 +1346,12 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
             const uint32_t nlen = co - ls, vlen = e - co - 3u;
             if constexpr (DENSE) {
               uint16_t *q = p.lens16 + hx;
-              fit = max(fit, max(nlen << 4, vlen));
+              const bool fits = max(nlen << 4, vlen) <= RHP_DENSE_VALUE_MAX;   /* name <= 62, value <= 1007 */
+              const uint32_t v16 = fits ? nlen | vlen << 6 : RHP_DENSE_OVERFLOW;
               if constexpr (decltype(wt_c)::value)
-                asm volatile("global_store_short %0, %1, off sc1" ::"v"(q), "v"(nlen | vlen << 6) : "memory");
-              else *GLOBAL(uint16_t, q) = (uint16_t) (nlen | vlen << 6);
+                asm volatile("global_store_short %0, %1, off sc1" ::"v"(q), "v"(v16) : "memory");
+              else *GLOBAL(uint16_t, q) = (uint16_t) v16;
+              if (!fits) *GLOBAL(uint32_t, p.ovf32 + hx) = nlen | vlen << 16;   /* rare: the overflow area */
             } else if constexpr (COMPACT) {
               uint32_t *q = p.lens + hx;
 #ifdef RHP_DIAG_NO_RECSTORE   /* diagnostic: the records computed, not stored (the stores' share) */
@@ -1379,10 +1392,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         const uint32_t e = base + (uint32_t) __builtin_ctz(eolm | 0x80000000u);
         const uint32_t co = t ? pco : base + (uint32_t) __builtin_ctz(com | 0x80000000u);
         const uint32_t lo = ls | ((co - ls) << 16), hi = (co + 2u) | ((e - co - 3u) << 16);
-        if constexpr (DENSE) {
-          store_len16_lanes(st_m, p.lens16 + hx, (co - ls) | ((e - co - 3u) << 6), wt);
-          fit = has ? max(fit, max((co - ls) << 4, e - co - 3u)) : fit;
-        } else if constexpr (COMPACT) store_len_lanes(st_m, p.lens + hx, (co - ls) | ((e - co - 3u) << 16), wt);
+        if constexpr (DENSE) store_dense_lanes(st_m, p, hx, co - ls, e - co - 3u, wt);
+        else if constexpr (COMPACT) store_len_lanes(st_m, p.lens + hx, (co - ls) | ((e - co - 3u) << 16), wt);
         else store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi}, wt);
         if (http) {   /* uniform: framing candidates only in http mode */
           const uint32_t nlen = co - ls;
@@ -1417,11 +1428,10 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       const uint32_t lo = ls | ((co - ls) << 16), hi = (co + 2u) | ((e - co - 3u) << 16);
       const uint64_t st_m = __builtin_amdgcn_ballot_w64(rec);
       if (st_m) {
-        if constexpr (DENSE) store_len16_lanes(st_m, p.lens16 + hx, (co - ls) | ((e - co - 3u) << 6), wt);
+        if constexpr (DENSE) store_dense_lanes(st_m, p, hx, co - ls, e - co - 3u, wt);
         else if constexpr (COMPACT) store_len_lanes(st_m, p.lens + hx, (co - ls) | ((e - co - 3u) << 16), wt);
         else store_rec_lanes(st_m, p.hdrs + hx, u32x2{lo, hi}, wt);
       }
-      if constexpr (DENSE) fit = rec ? max(fit, max((co - ls) << 4, e - co - 3u)) : fit;
       if (http) {
         const uint32_t nlen = co - ls;
         const bool cnd = rec && (nlen == 14u || nlen == 17u);
@@ -1635,9 +1645,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       }
     }
     /* dense records (phr mode): a DFA record whose method is longer than 255
-     * bytes or one of whose header records does not fit the 2-byte form takes
-     * the exact path (the wide records) */
-    if constexpr (DENSE) ok = ok && (rl & 0xffffu) <= 255u && fit <= RHP_DENSE_VALUE_MAX;
+     * bytes takes the exact path (the wide records) */
+    if constexpr (DENSE) ok = ok && (rl & 0xffffu) <= 255u;
     /* the record as four dwords (rhp.h rhp_req_t: ret; method_len, path_off;
      * path_len, method_off 0, minor_version; num_headers, flags) */
     u32x4 rq = u32x4{0u, 0u, 0xff000000u, 0u};   /* minor_version -1 */
@@ -2078,14 +2087,16 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (any_walk) {
         if (!walking) st = kPark;
         zero_lead(wnew);
+#ifndef RHP_DIAG_NO_WALK   /* diagnostic builds only (see the early form) */
         walk();
+#endif
       }
       dg.section(3, true);
       if (walking && wnew) {
         dcur = wcur;
         dlen = wlen;
         doff = woff;
-        kn = me = pe = rl = nh = ls = t = pco = ovf = fit = 0;
+        kn = me = pe = rl = nh = ls = t = pco = ovf = 0;
         cand = wget;
         crec_lo = crec_hi = 0;
         fr = 0;
@@ -2098,9 +2109,13 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       for (int w = 0; w < (int) kWEv; w++) evp[w] = ev[w];
       decode_begin();
       const uint32_t crec_before = crec_lo | (cand & 0xbfffffffu);
+#ifndef RHP_DIAG_NO_DECODE   /* diagnostic builds only (see the early form) */
       if (any_walk) decode_window();
+#endif
       dg.section(kSecDecodeStamp, true);
+#ifndef RHP_DIAG_NO_FRAME   /* diagnostic builds only: the in-loop framing's share */
       if (http && any_walk) frame_window(crec_before);
+#endif
       dg.section(kSecFrameStamp, true);
       const bool done = any_walk ? decode_end() : false;
       dg.section(2, true);
@@ -2127,7 +2142,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         dcur = wcur;
         dlen = wlen;
         if constexpr (LATE) doff = woff;
-        kn = me = pe = rl = nh = ls = t = pco = ovf = fit = 0;
+        kn = me = pe = rl = nh = ls = t = pco = ovf = 0;
         cand = wget;
         crec_lo = crec_hi = 0;
       }
@@ -2511,7 +2526,8 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   if (b->mode != RHP_MODE_PHR && b->mode != RHP_MODE_HTTP) return -22;
   if (b->layout != RHP_LAYOUT_REQUEST_MAJOR && b->layout != RHP_LAYOUT_HEADER_MAJOR &&
       !(b->layout == RHP_LAYOUT_COMPACT && !(b->flags & RHP_BATCH_SPECULATIVE)) &&
-      !(b->layout == RHP_LAYOUT_DENSE && b->mode == RHP_MODE_PHR)) return -22;   /* compact: not speculative; dense: phr */
+      !((b->layout == RHP_LAYOUT_DENSE || b->layout == RHP_LAYOUT_DENSE_RM) && b->mode == RHP_MODE_PHR))
+    return -22;   /* compact: not speculative; dense: phr */
   if (b->last_len && b->mode != RHP_MODE_PHR) return -22;   /* http_read_request passes last_len 0 */
   if ((b->flags & ~RHP_BATCH_SPECULATIVE) || ((b->flags & RHP_BATCH_SPECULATIVE) && b->mode != RHP_MODE_HTTP)) return -22;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -2538,25 +2554,29 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   prm.mode = b->mode;
   prm.span = 0;
   const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR;
-  const bool compact = b->layout == RHP_LAYOUT_COMPACT, dense = b->layout == RHP_LAYOUT_DENSE;
+  const bool compact = b->layout == RHP_LAYOUT_COMPACT;
+  const bool dense = b->layout == RHP_LAYOUT_DENSE || b->layout == RHP_LAYOUT_DENSE_RM;
   prm.hs_req = hmajor ? 1u : b->max_headers;
   prm.hs_hdr = hmajor ? b->n : 1u;
   prm.lens = nullptr;
   prm.hc = nullptr;
   prm.dreq = nullptr;
   prm.lens16 = nullptr;
+  prm.ovf32 = nullptr;
   prm.rec_req = prm.hs_req;
   prm.rec_hdr = prm.hs_hdr;
-  prm.wt_records = b->mode == RHP_MODE_PHR && b->layout != RHP_LAYOUT_REQUEST_MAJOR;
+  prm.wt_records = b->mode == RHP_MODE_PHR && b->layout != RHP_LAYOUT_REQUEST_MAJOR && b->layout != RHP_LAYOUT_DENSE_RM;
   if (dense) {   /* 8-byte request records and u16 lengths (header-major), the wide ones behind them */
     prm.dreq = reinterpret_cast<uint2 *>(b->reqs);
     prm.reqs = reinterpret_cast<rhp_req_t *>(reinterpret_cast<uint8_t *>(b->reqs) + RHP_DENSE_REQ_WIDE_OFF(b->n));
     prm.lens16 = reinterpret_cast<uint16_t *>(b->hdrs);
+    prm.ovf32 = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(b->hdrs) + RHP_DENSE_OVF_OFF(b->n, b->max_headers));
     prm.hdrs = reinterpret_cast<rhp_hdr_t *>(reinterpret_cast<uint8_t *>(b->hdrs) + RHP_DENSE_WIDE_OFF(b->n, b->max_headers));
     prm.hs_req = b->max_headers;   /* the exact path's wide records: request-major */
     prm.hs_hdr = 1u;
-    prm.rec_req = 1u;
-    prm.rec_hdr = b->n;
+    const bool rm = b->layout == RHP_LAYOUT_DENSE_RM;   /* the u16 lengths request-major or header-major */
+    prm.rec_req = rm ? b->max_headers : 1u;
+    prm.rec_hdr = rm ? 1u : b->n;
   }
   if (compact) {   /* lengths header-major at hdrs, the wide records request-major behind them */
     prm.lens = reinterpret_cast<uint32_t *>(b->hdrs);

@@ -1,12 +1,13 @@
-"""Dense records (RHP_LAYOUT_DENSE, include/rhp.h; round 6): 8-byte request
-records and 2-byte header lengths for what the DFA parses, the wide rhp_req_t /
-rhp_hdr_t records for everything else.  Expanded (rhp_expand_reqs,
-rhp_expand_records), the records equal the reference's (golden fixtures, the
-oracle, full-size digests) whichever path parsed a request.
+"""Dense records (RHP_LAYOUT_DENSE / RHP_LAYOUT_DENSE_RM, include/rhp.h; round
+6): 8-byte request records and 2-byte header lengths (header- or request-major)
+for what the DFA parses, the wide rhp_req_t / rhp_hdr_t records for everything
+else.  Expanded (rhp_expand_reqs, rhp_expand_records), the records equal the
+reference's (golden fixtures, the oracle, full-size digests) whichever path
+parsed a request.
 
-CPU: the kernel's emulator and the product's exact parser in the dense layout;
-the fields the dense form cannot hold (a method over 255 bytes, a header name
-of 63+ or a value of 1008+ bytes) send a request to the exact path.
+CPU: the kernel's emulator and the product's exact parser in the dense layouts;
+a method over 255 bytes sends a request to the exact path, a header name of 63+
+or a value of 1008+ bytes overflows into the u32 area.
 GPU (-m gpu): the DFA kernel (both loop forms) and the exact kernel in the dense
 layout, against the golden sets, fuzz at every max_headers, the full-size
 digests of configs 2/3/4, edge cases at every alignment, last_len; the
@@ -28,6 +29,7 @@ SETS = json.load(open(os.path.join(GOLDEN, "manifest.json")))["sets"]
 FULL = json.load(open(os.path.join(GOLDEN, "full_digests.json")))["sets"]
 PHR_SETS = sorted(k for k, v in SETS.items() if v["mode"] == rhp.MODE_PHR)
 D = rhp.LAYOUT_DENSE
+LAYS = [rhp.LAYOUT_DENSE, rhp.LAYOUT_DENSE_RM]
 
 
 def golden(name):
@@ -57,26 +59,33 @@ def long_fields():
             b"GET / HTTP/1.1\r\nA: b\r\n"]                                      # -2: exact
 
 
+@pytest.mark.parametrize("lay", LAYS)
 @pytest.mark.parametrize("name", PHR_SETS)
-def test_emulation_dense_matches_golden(name):
+def test_emulation_dense_matches_golden(name, lay):
     spec, buf, off, want = golden(name)
-    res, _ = rhp.emulate(buf, off, spec["max_headers"], spec["mode"], D)
-    assert_same(canon(res, spec["mode"]), want, buf, off, f"emulation (dense) vs golden {name}")
-    res = rhp.parse_cpu_exact(buf, off, spec["max_headers"], spec["mode"], D)
+    res, _ = rhp.emulate(buf, off, spec["max_headers"], spec["mode"], lay)
+    assert_same(canon(res, spec["mode"]), want, buf, off, f"emulation (dense {lay}) vs golden {name}")
+    res = rhp.parse_cpu_exact(buf, off, spec["max_headers"], spec["mode"], lay)
     assert_same(canon(res, spec["mode"]), want, buf, off, f"CPU exact (dense) vs golden {name}")
     flags, _ = dense_fields(res, len(off) - 1)
     assert (flags & rhp.DENSE_WIDE).all()   # the exact parser's records are all wide
 
 
-def test_dense_field_limits_take_the_exact_path():
+@pytest.mark.parametrize("lay", LAYS)
+def test_dense_field_limits(lay):
     buf, off = pack(long_fields())
     want = to_rhp(*run_oracle(buf, off, 16, rhp.MODE_PHR)[:3], rhp.MODE_PHR)
-    res, _ = rhp.emulate(buf, off, 16, rhp.MODE_PHR, D)
+    res, _ = rhp.emulate(buf, off, 16, rhp.MODE_PHR, lay)
     assert_same(canon(res, rhp.MODE_PHR), want, buf, off, "dense limits (emulation)")
     flags, _ = dense_fields(res, len(off) - 1)
     wide = (flags & rhp.DENSE_WIDE) != 0
-    assert list(wide) == [False, True, False, True, False, True, False, False, False, True]
+    # a long method takes the exact path; long names and values overflow into the u32 area
+    assert list(wide) == [False, True, False, False, False, False, False, False, False, True]
     assert flags[8] & rhp.DENSE_BAD
+    n = len(off) - 1
+    l16 = res.raw_hdrs[: 2 * n * 16].view(np.uint16)
+    k0 = (np.arange(n) * 16) if lay == rhp.LAYOUT_DENSE_RM else np.arange(n)   # header 0 of each request
+    assert list(l16[k0] == 0xFFFF) == [False, False, False, True, False, True, False, False, False, False]
 
 
 def test_dense_rejected_outside_phr_mode():
@@ -89,8 +98,8 @@ def test_dense_rejected_outside_phr_mode():
 
 def test_dense_sizes():
     assert rhp.reqs_bytes(1000, D) == 8000 + 16000
-    assert rhp.hdrs_bytes(1000, 16, D) == 32000 + 128000
-    assert rhp.hdrs_bytes(3, 3, D) == 32 + 72   # the wide area 16-byte aligned
+    assert rhp.hdrs_bytes(1000, 16, D) == 32000 + 64000 + 128000
+    assert rhp.hdrs_bytes(3, 3, D) == 32 + 48 + 72   # the areas 16-byte aligned
 
 
 # ------------------------------------------------------------------ GPU
@@ -99,45 +108,49 @@ IMPLS = [rhp.IMPL_DFA, rhp.IMPL_DFA_LATE, rhp.IMPL_EXACT]
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lay", LAYS)
 @pytest.mark.parametrize("impl", IMPLS)
 @pytest.mark.parametrize("name", PHR_SETS)
-def test_gpu_dense_matches_reference_golden(name, impl):
+def test_gpu_dense_matches_reference_golden(name, impl, lay):
     spec, buf, off, want = golden(name)
-    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], impl=impl, layout=D)
+    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], impl=impl, layout=lay)
     assert_same(canon(res, spec["mode"]), want, buf, off, f"GPU dense impl{impl} vs golden {name}")
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lay", LAYS)
 @pytest.mark.parametrize("maxh", [0, 1, 3, 16, 32, 64])
-def test_gpu_dense_fuzz_vs_oracle(maxh):
+def test_gpu_dense_fuzz_vs_oracle(maxh, lay):
     for impl, seed in ((rhp.IMPL_DFA, 9600 + maxh), (rhp.IMPL_DFA_LATE, 9700 + maxh)):
         buf, off = rhp.generate(rhp.GEN_FUZZ, 60000, seed)
-        res = rhp.parse_batch(buf, off, maxh, rhp.MODE_PHR, impl=impl, layout=D)
+        res = rhp.parse_batch(buf, off, maxh, rhp.MODE_PHR, impl=impl, layout=lay)
         want = to_rhp(*run_oracle(buf, off, maxh, rhp.MODE_PHR)[:3], rhp.MODE_PHR)
         assert_same(canon(res, rhp.MODE_PHR), want, buf, off, f"GPU dense fuzz impl{impl} maxh{maxh}")
-        emu, _ = rhp.emulate(buf, off, maxh, rhp.MODE_PHR, D)
+        emu, _ = rhp.emulate(buf, off, maxh, rhp.MODE_PHR, lay)
         assert np.array_equal(res.reqs["flags"] & (rhp.F_EXACT | rhp.F_WIDE), emu.reqs["flags"] & (rhp.F_EXACT | rhp.F_WIDE))
 
 
 @pytest.mark.gpu
-def test_gpu_dense_field_limits():
+@pytest.mark.parametrize("lay", LAYS)
+def test_gpu_dense_field_limits(lay):
     buf, off = pack(long_fields() * 40)
     want = to_rhp(*run_oracle(buf, off, 16, rhp.MODE_PHR)[:3], rhp.MODE_PHR)
     for impl in IMPLS:
-        res = rhp.parse_batch(buf, off, 16, rhp.MODE_PHR, impl=impl, layout=D)
+        res = rhp.parse_batch(buf, off, 16, rhp.MODE_PHR, impl=impl, layout=lay)
         assert_same(canon(res, rhp.MODE_PHR), want, buf, off, f"GPU dense limits impl{impl}")
-    emu, _ = rhp.emulate(buf, off, 16, rhp.MODE_PHR, D)
-    res = rhp.parse_batch(buf, off, 16, rhp.MODE_PHR, layout=D)
+    emu, _ = rhp.emulate(buf, off, 16, rhp.MODE_PHR, lay)
+    res = rhp.parse_batch(buf, off, 16, rhp.MODE_PHR, layout=lay)
     assert np.array_equal(dense_fields(res, len(off) - 1)[0], dense_fields(emu, len(off) - 1)[0])
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lay", LAYS)
 @pytest.mark.parametrize("name", ["config2_get256_h16", "config3_zipf_h32", "config4_get256_shard5of8",
                                   "config4_get256_shard7of8"])
-def test_gpu_dense_full_size_matches_reference_digest(name):
+def test_gpu_dense_full_size_matches_reference_digest(name, lay):
     spec = FULL[name]
     buf, off = inputs(spec)
-    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], layout=D)
+    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], layout=lay)
     got = canon(res, spec["mode"])
     if record_digest(*got) != spec["records_sha256"]:
         want = to_rhp(*run_oracle(buf, off, spec["max_headers"], spec["mode"])[:3], spec["mode"])
@@ -146,20 +159,22 @@ def test_gpu_dense_full_size_matches_reference_digest(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lay", LAYS)
 @pytest.mark.parametrize("shift", [0, 1, 2, 3])
-def test_gpu_dense_edge_cases(shift):
+def test_gpu_dense_edge_cases(shift, lay):
     buf, off = pack(EDGE * 3, align_shift=shift)
     for maxh in (0, 1, 16):
         want = to_rhp(*run_oracle(buf, off, maxh, rhp.MODE_PHR)[:3], rhp.MODE_PHR)
-        res = rhp.parse_batch(buf, off, maxh, rhp.MODE_PHR, layout=D)
+        res = rhp.parse_batch(buf, off, maxh, rhp.MODE_PHR, layout=lay)
         assert_same(canon(res, rhp.MODE_PHR), want, buf, off, f"GPU dense edge shift{shift} maxh{maxh}")
 
 
 @pytest.mark.gpu
-def test_gpu_dense_last_len_matches_reference_golden():
+@pytest.mark.parametrize("lay", LAYS)
+def test_gpu_dense_last_len_matches_reference_golden(lay):
     top = json.load(open(os.path.join(GOLDEN, "manifest.json")))
     buf, off = inputs(top["phr_last_len"])
     z = np.load(os.path.join(GOLDEN, "phr_last_len.npz"))
     for impl in IMPLS:
-        res = rhp.parse_batch(buf, off, 16, rhp.MODE_PHR, impl=impl, layout=D, last_len=z["last_len"])
+        res = rhp.parse_batch(buf, off, 16, rhp.MODE_PHR, impl=impl, layout=lay, last_len=z["last_len"])
         assert_same(canon(res, rhp.MODE_PHR), (z["reqs"], z["hdrs"], None), buf, off, f"GPU dense impl{impl} last_len")

@@ -7,6 +7,7 @@
 #   quick  the GPU tests whose names match TESTS_K (pytest -k)
 #   lines  tools/ubench_lines (window line order vs bandwidth; built beforehand)
 #   ab     tools/ab_libs.py over AB_LIBS ("tag=path ...") for each of AB_CONFIGS
+#   stamps tools/stamps2.py on the RHP_STAMPS build (librhp_x_stamps.so) for STAMPS_CFG
 # (round 6: one script for every session; the per-session env is recorded in
 # the profiles README that keeps its output)
 set -o pipefail
@@ -70,11 +71,15 @@ step_ab() {
     grep "^ab $c\|parity" gpurun_out/ab_${TAG}_$c.txt
   done
 }
+step_stamps() {
+  RHP_LIB=$PWD/libreactorng_amd/librhp_x_stamps.so timeout -k 10 300 python3 tools/stamps2.py > gpurun_out/stamps_${TAG}.txt 2>&1 \
+    && grep -v Warning gpurun_out/stamps_${TAG}.txt | head -40
+}
 step_smoke() {
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" > gpurun_out/smoke_${TAG}.log 2>&1 \
     && tail -1 gpurun_out/smoke_${TAG}.log
 }
-( ! has quick || step_quick ) && ( ! has lines || step_lines ) && ( ! has ab || step_ab ) \
+( ! has quick || step_quick ) && ( ! has lines || step_lines ) && ( ! has ab || step_ab ) && ( ! has stamps || step_stamps ) \
   && ( ! has tests || step_tests ) && ( ! has bench || step_bench ) && ( ! has prof || step_prof ) && ( ! has pmc || step_pmc ) \
   && ( ! has sq || step_sq ) && ( ! has writer || step_writer ) && ( ! has smoke || step_smoke ) \
   && ( ! has ceil || step_ceil ) && echo SESSION_OK

@@ -356,7 +356,7 @@ def http_bytes(n: int, mode: int, layout: int) -> int:
     """bytes the batch's http buffer needs (rhp.h; RHP_COMPACT_HTTP_BYTES for the compact layout)"""
     if mode != MODE_HTTP:
         return HTTP_DTYPE.itemsize
-    if layout == LAYOUT_COMPACT:
+    if layout in (LAYOUT_COMPACT, LAYOUT_DENSE):   # compact http records and their wide area
         return ((n * 8 + 15) & ~15) + n * HTTP_DTYPE.itemsize
     return n * HTTP_DTYPE.itemsize
 
@@ -365,7 +365,7 @@ def expand_http(reqs: np.ndarray, raw: np.ndarray, n: int, layout: int) -> np.nd
     """[n] rhp_http_t records of a parsed http batch from its raw http bytes in any
     layout (rhp_expand_http, include/rhp_host.h: compact records expanded)."""
     raw = np.ascontiguousarray(raw).view(np.uint8)
-    if layout != LAYOUT_COMPACT:
+    if layout not in (LAYOUT_COMPACT, LAYOUT_DENSE):
         return raw[: n * HTTP_DTYPE.itemsize].view(HTTP_DTYPE).copy()
     out = np.zeros(n, dtype=HTTP_DTYPE)
     if n == 0:

@@ -54,7 +54,10 @@ rhp_hdr_t *wide_records(const rhp_batch_t *b, uint32_t i, uint64_t &hs_hdr)
 /* compact http records (rhp.h, RHP_LAYOUT_COMPACT in http mode): as the kernel,
  * a record whose consumed follows from ret is stored compact, any other one
  * (the exact path's, a chunked body de-framed in place) in the wide area */
-bool compact_http(const rhp_batch_t *b) { return b->mode == RHP_MODE_HTTP && b->layout == RHP_LAYOUT_COMPACT; }
+bool compact_http(const rhp_batch_t *b)
+{
+  return b->mode == RHP_MODE_HTTP && (b->layout == RHP_LAYOUT_COMPACT || b->layout == RHP_LAYOUT_DENSE);
+}
 rhp_http_compact_t *http_compact(const rhp_batch_t *b) { return reinterpret_cast<rhp_http_compact_t *>(b->http); }
 rhp_http_t *http_wide(const rhp_batch_t *b)
 {
@@ -133,7 +136,7 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
 {
   if ((b->layout == RHP_LAYOUT_COMPACT || dense_layout(b)) && (b->flags & RHP_BATCH_SPECULATIVE))
     return -22;   /* as rhp_parse_batch */
-  if (dense_layout(b) && b->mode != RHP_MODE_PHR) return -22;
+  if (b->layout == RHP_LAYOUT_DENSE_RM && b->mode != RHP_MODE_PHR) return -22;   /* dense http: header-major */
   const Table2 &T = table();
   const uint8_t *cls = T.b + kClassRow * 256u;
   Stats st_count = {0, 0, 0};
@@ -165,6 +168,12 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
                                   (drm ? (uint64_t) i * maxh : i)
                             : nullptr;
     const uint64_t dstride = drm ? 1u : b->n;
+    /* header k's u32 lengths, name_len | value_len << 16, in the compact or a dense layout */
+    auto len32 = [&](uint32_t k) -> uint32_t {
+      if (compact) return lens[(uint64_t) k * b->n];
+      const uint32_t l = lens16[k * dstride];
+      return l == RHP_DENSE_OVERFLOW ? ovf32[k * dstride] : (l & 63u) | (l >> 6) << 16;
+    };
     /* the kernel's window: http mode walks RHP_HTTP_BLOCK bytes per window */
     const int32_t block = b->mode == RHP_MODE_HTTP ? RHP_HTTP_BLOCK : RHP_BLOCK;
     constexpr int kMaxWords = (RHP_HTTP_BLOCK > RHP_BLOCK ? RHP_HTTP_BLOCK : RHP_BLOCK) / 32;
@@ -254,7 +263,7 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
                                              (uint8_t) r.minor_version, 0};
         else
           b->reqs[i] = r;
-        if (b->mode == RHP_MODE_HTTP && compact) {
+        if (b->mode == RHP_MODE_HTTP && (compact || dense)) {
           /* as the kernel: with compact records a request that is not GET and
            * has three or more framing candidates (names of 14 or 17 bytes), or
            * one at header index >= 30, is framed by the exact path (its http_frame
@@ -262,7 +271,7 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
           uint32_t ncand = 0;
           bool late = false;
           for (uint32_t k = 0; k < d.nh && k < maxh; k++) {
-            const uint32_t nl = lens[(uint64_t) k * b->n] & 0xffffu;
+            const uint32_t nl = len32(k) & 0xffffu;
             if (nl == 14u || nl == 17u) {
               ncand++;
               late |= k >= 30u;
@@ -278,11 +287,11 @@ extern "C" int rhp_emu_parse_batch(const rhp_batch_t *b, uint64_t *stats /* [3] 
         }
         if (b->mode == RHP_MODE_HTTP) {
           rhp_http_t x;
-          if (compact) {   /* http_frame reads rhp_hdr_t records: the lengths expanded */
+          if (compact || dense) {   /* http_frame reads rhp_hdr_t records: the lengths expanded */
             rhp_hdr_t tmp[RHP_MAX_HEADERS];
             uint32_t at = (uint32_t) r.path_off + r.path_len + 11u;
             for (uint32_t k = 0; k < d.nh && k < maxh; k++) {
-              const uint32_t l = lens[(uint64_t) k * b->n], nl = l & 0xffffu, vl = l >> 16;
+              const uint32_t l = len32(k), nl = l & 0xffffu, vl = l >> 16;
               tmp[k] = rhp_hdr_t{(uint16_t) at, (uint16_t) nl, (uint16_t) (at + nl + 2u), (uint16_t) vl};
               at += nl + vl + 4u;
             }
@@ -433,7 +442,7 @@ extern "C" int rhp_expand_reqs(const rhp_batch_t *b, const void *reqs, rhp_req_t
 extern "C" int rhp_expand_http(const rhp_batch_t *b, const rhp_req_t *reqs, const void *http, rhp_http_t *out)
 {
   if (!b || !reqs || !http || !out) return -22;
-  if (b->layout != RHP_LAYOUT_COMPACT) {
+  if (b->layout != RHP_LAYOUT_COMPACT && b->layout != RHP_LAYOUT_DENSE) {
     memcpy(out, http, sizeof(rhp_http_t) * b->n);
     return 0;
   }
@@ -473,7 +482,8 @@ extern "C" int rhp_cpu_parse_batch(const rhp_batch_t *b)
   /* as rhp_parse_batch: compact records in both modes (every record wide: the
    * exact path's), not in a speculative batch */
   if (b->layout == RHP_LAYOUT_COMPACT && (b->flags & RHP_BATCH_SPECULATIVE)) return -22;
-  if (dense_layout(b) && (b->mode != RHP_MODE_PHR || (b->flags & RHP_BATCH_SPECULATIVE))) return -22;
+  if (dense_layout(b) && ((b->layout == RHP_LAYOUT_DENSE_RM && b->mode != RHP_MODE_PHR) || (b->flags & RHP_BATCH_SPECULATIVE)))
+    return -22;
   for (uint32_t i = 0; i < b->n; i++) emu_exact(b, i, b->offsets[i], b->offsets[i + 1] - b->offsets[i]);
   return 0;
 }

@@ -1043,7 +1043,6 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
 {
   constexpr bool COMPACT = REC != kRecWide;   /* lengths, offsets by the running sum */
   constexpr bool DENSE = REC == kRecDense;
-  static_assert(!(DENSE && HTTP), "dense records: phr mode only");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
@@ -2231,14 +2230,21 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
      * the compact layout, summed from the lengths after the first one's */
     auto frame_fast = [&](uint32_t i, const Head &h) {
       const uint32_t cand = h.hint[0], crec_hi = h.hint[3];
+      /* header k's u32 lengths (compact), or from the dense u16 / its overflow area */
+      auto len32 = [&](uint32_t k) -> uint32_t {
+        const uint64_t at = (uint64_t) k * p.rec_hdr + (uint64_t) i * p.rec_req;
+        if constexpr (!DENSE) return p.lens[at];
+        const uint32_t l = p.lens16[at];
+        return l == RHP_DENSE_OVERFLOW ? p.ovf32[at] : (l & 63u) | (l >> 6) << 16;
+      };
       auto rec = [&](uint32_t j) -> uint2 {
         if (!p.hc) return *reinterpret_cast<const uint2 *>(p.hdrs + (uint64_t) i * p.hs_req + (uint64_t) j * p.hs_hdr);
         uint32_t at = (crec_hi & 0xffffu) + (crec_hi >> 16) + 2u;   /* the line after the first candidate's */
         for (uint32_t k = (uint32_t) __builtin_ctz(cand & 0x3fffffffu) + 1u; k < j; k++) {
-          const uint32_t l = p.lens[(uint64_t) k * p.rec_hdr + i];
+          const uint32_t l = len32(k);
           at += (l & 0xffffu) + (l >> 16) + 4u;
         }
-        const uint32_t l = p.lens[(uint64_t) j * p.rec_hdr + i];
+        const uint32_t l = len32(j);
         return uint2{at | (l & 0xffffu) << 16, (at + (l & 0xffffu) + 2u) | (l >> 16) << 16};
       };
       rhp_http_t o;
@@ -2526,8 +2532,8 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   if (b->mode != RHP_MODE_PHR && b->mode != RHP_MODE_HTTP) return -22;
   if (b->layout != RHP_LAYOUT_REQUEST_MAJOR && b->layout != RHP_LAYOUT_HEADER_MAJOR &&
       !(b->layout == RHP_LAYOUT_COMPACT && !(b->flags & RHP_BATCH_SPECULATIVE)) &&
-      !((b->layout == RHP_LAYOUT_DENSE || b->layout == RHP_LAYOUT_DENSE_RM) && b->mode == RHP_MODE_PHR))
-    return -22;   /* compact: not speculative; dense: phr */
+      !(b->layout == RHP_LAYOUT_DENSE || b->layout == RHP_LAYOUT_DENSE_RM))
+    return -22;   /* compact: not speculative; dense: below */
   if (b->last_len && b->mode != RHP_MODE_PHR) return -22;   /* http_read_request passes last_len 0 */
   if ((b->flags & ~RHP_BATCH_SPECULATIVE) || ((b->flags & RHP_BATCH_SPECULATIVE) && b->mode != RHP_MODE_HTTP)) return -22;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -2556,6 +2562,8 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   const bool hmajor = b->layout == RHP_LAYOUT_HEADER_MAJOR;
   const bool compact = b->layout == RHP_LAYOUT_COMPACT;
   const bool dense = b->layout == RHP_LAYOUT_DENSE || b->layout == RHP_LAYOUT_DENSE_RM;
+  if (dense && (b->mode == RHP_MODE_HTTP ? b->layout != RHP_LAYOUT_DENSE || (b->flags & RHP_BATCH_SPECULATIVE) : false))
+    return -22;   /* http mode: header-major dense records, not speculative */
   prm.hs_req = hmajor ? 1u : b->max_headers;
   prm.hs_hdr = hmajor ? b->n : 1u;
   prm.lens = nullptr;
@@ -2577,6 +2585,10 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
     const bool rm = b->layout == RHP_LAYOUT_DENSE_RM;   /* the u16 lengths request-major or header-major */
     prm.rec_req = rm ? b->max_headers : 1u;
     prm.rec_hdr = rm ? 1u : b->n;
+    if (b->mode == RHP_MODE_HTTP) {   /* the compact http records, as RHP_LAYOUT_COMPACT's */
+      prm.hc = reinterpret_cast<uint2 *>(b->http);
+      prm.http = reinterpret_cast<rhp_http_t *>(reinterpret_cast<uint8_t *>(b->http) + RHP_COMPACT_HTTP_WIDE_OFF(b->n));
+    }
   }
   if (compact) {   /* lengths header-major at hdrs, the wide records request-major behind them */
     prm.lens = reinterpret_cast<uint32_t *>(b->hdrs);
@@ -2599,8 +2611,9 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   }
   const bool late = late_issue(b->mode);
   if (b->mode == RHP_MODE_HTTP)
-    return compact ? launch_dfa<kHttpWaves, true, true, kRecCompact>(prm, s, dev, cus)
-                   : launch_dfa<kHttpWaves, true, true, kRecWide>(prm, s, dev, cus);
+    return dense     ? launch_dfa<kHttpWaves, true, true, kRecDense>(prm, s, dev, cus)
+           : compact ? launch_dfa<kHttpWaves, true, true, kRecCompact>(prm, s, dev, cus)
+                     : launch_dfa<kHttpWaves, true, true, kRecWide>(prm, s, dev, cus);
   if (dense) return late ? launch_dfa<16, true, false, kRecDense>(prm, s, dev, cus) : launch_dfa<16, false, false, kRecDense>(prm, s, dev, cus);
   if (compact) return late ? launch_dfa<16, true, false, kRecCompact>(prm, s, dev, cus) : launch_dfa<16, false, false, kRecCompact>(prm, s, dev, cus);
   if (late) return launch_dfa<16, true, false, kRecWide>(prm, s, dev, cus);

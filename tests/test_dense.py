@@ -28,6 +28,7 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 SETS = json.load(open(os.path.join(GOLDEN, "manifest.json")))["sets"]
 FULL = json.load(open(os.path.join(GOLDEN, "full_digests.json")))["sets"]
 PHR_SETS = sorted(k for k, v in SETS.items() if v["mode"] == rhp.MODE_PHR)
+HTTP_SETS = sorted(k for k, v in SETS.items() if v["mode"] == rhp.MODE_HTTP)
 D = rhp.LAYOUT_DENSE
 LAYS = [rhp.LAYOUT_DENSE, rhp.LAYOUT_DENSE_RM]
 
@@ -36,7 +37,7 @@ def golden(name):
     spec = SETS[name]
     buf, off = inputs(spec)
     z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
-    return spec, buf, off, (z["reqs"], z["hdrs"], None)
+    return spec, buf, off, (z["reqs"], z["hdrs"], z["http"] if "http" in z.files else None)
 
 
 def dense_fields(res, n):
@@ -88,12 +89,25 @@ def test_dense_field_limits(lay):
     assert list(l16[k0] == 0xFFFF) == [False, False, False, True, False, True, False, False, False, False]
 
 
-def test_dense_rejected_outside_phr_mode():
+def test_dense_request_major_rejected_in_http_mode():
     buf, off = pack([b"GET / HTTP/1.1\r\n\r\n"])
     with pytest.raises(RuntimeError):
-        rhp.emulate(buf, off, 16, rhp.MODE_HTTP, D)
+        rhp.emulate(buf, off, 16, rhp.MODE_HTTP, rhp.LAYOUT_DENSE_RM)
     with pytest.raises(RuntimeError):
-        rhp.parse_cpu_exact(buf, off, 16, rhp.MODE_HTTP, D)
+        rhp.parse_cpu_exact(buf, off, 16, rhp.MODE_HTTP, rhp.LAYOUT_DENSE_RM)
+
+
+@pytest.mark.parametrize("name", HTTP_SETS)
+def test_emulation_dense_http_matches_golden(name):
+    """http mode (round 6): dense request and header records beside the compact
+    http records; de-framed bytes as the reference's"""
+    spec, buf, off, want = golden(name)
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    for res in (rhp.emulate(buf, off, spec["max_headers"], spec["mode"], D)[0],
+                rhp.parse_cpu_exact(buf, off, spec["max_headers"], spec["mode"], D)):
+        assert_same(canon(res, spec["mode"]), want, buf, off, f"dense http vs golden {name}")
+        if "bytes_out_sha256" in z.files:
+            assert hashlib.sha256(res.bytes_out.tobytes()).digest() == z["bytes_out_sha256"].tobytes()
 
 
 def test_dense_sizes():
@@ -178,3 +192,42 @@ def test_gpu_dense_last_len_matches_reference_golden(lay):
     for impl in IMPLS:
         res = rhp.parse_batch(buf, off, 16, rhp.MODE_PHR, impl=impl, layout=lay, last_len=z["last_len"])
         assert_same(canon(res, rhp.MODE_PHR), (z["reqs"], z["hdrs"], None), buf, off, f"GPU dense impl{impl} last_len")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("impl", [rhp.IMPL_DFA, rhp.IMPL_EXACT])
+@pytest.mark.parametrize("name", HTTP_SETS)
+def test_gpu_dense_http_matches_reference_golden(name, impl):
+    spec, buf, off, want = golden(name)
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"))
+    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], impl=impl, layout=D)
+    assert_same(canon(res, spec["mode"]), want, buf, off, f"GPU dense http impl{impl} vs golden {name}")
+    if "bytes_out_sha256" in z.files:
+        assert hashlib.sha256(res.bytes_out.tobytes()).digest() == z["bytes_out_sha256"].tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("maxh", [0, 1, 3, 16, 32, 64])
+def test_gpu_dense_http_fuzz_vs_oracle(maxh):
+    buf, off = rhp.generate(rhp.GEN_FUZZ_HTTP, 60000, 9800 + maxh)
+    res = rhp.parse_batch(buf, off, maxh, rhp.MODE_HTTP, layout=D)
+    rq, hd, ht, out = run_oracle(buf, off, maxh, rhp.MODE_HTTP)
+    assert_same(canon(res, rhp.MODE_HTTP), to_rhp(rq, hd, ht, rhp.MODE_HTTP), buf, off, f"GPU dense http fuzz maxh{maxh}")
+    assert (res.bytes_out == out).all()
+    emu, _ = rhp.emulate(buf, off, maxh, rhp.MODE_HTTP, D)
+    assert np.array_equal(res.reqs["flags"] & (rhp.F_EXACT | rhp.F_WIDE), emu.reqs["flags"] & (rhp.F_EXACT | rhp.F_WIDE))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["config5_post1k_http_h16", "chunked_post_http_h16"])
+def test_gpu_dense_http_full_size_matches_reference_digest(name):
+    spec = FULL[name]
+    buf, off = inputs(spec)
+    res = rhp.parse_batch(buf, off, spec["max_headers"], spec["mode"], layout=D)
+    got = canon(res, spec["mode"])
+    if record_digest(*got) != spec["records_sha256"]:
+        want = to_rhp(*run_oracle(buf, off, spec["max_headers"], spec["mode"])[:3], spec["mode"])
+        assert_same(got, want, buf, off, name)
+        raise AssertionError(f"{name}: dense digest differs from the reference but matches the oracle")
+    if "bytes_out_sha256" in spec:
+        assert hashlib.sha256(res.bytes_out.tobytes()).hexdigest() == spec["bytes_out_sha256"]

@@ -1559,24 +1559,22 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       /* strtoull (rhp_scalar.h num_step) over the value bytes: a fast-path
        * value starts with neither OWS nor a CTL, so only the sign and the
        * digit run matter; up to 12 bytes per window here, more -> the replay */
-      uint32_t v5[3];
-#pragma unroll
-      for (uint32_t k = 0; k < 3; k++) v5[k] = fresh ? d[4 + k] : d[k];
+      /* one byte per trip, straight-line (selects, no exec-masked branches: the
+       * branchy form spent ~25 scalar instructions per trip on exec masks); the
+       * 12 value bytes shift down a byte per trip */
+      uint32_t w0 = fresh ? d[4] : d[0], w1 = fresh ? d[5] : d[1], w2 = fresh ? d[6] : d[2];
       const uint32_t m = min(n, 12u);
       for (uint32_t j = 0; __builtin_amdgcn_ballot_w64(j < m && !(fr & kFrStop)); j++) {
-        if (j < m && !(fr & kFrStop)) {
-          const uint32_t w = j < 4u ? v5[0] : j < 8u ? v5[1] : v5[2];
-          const uint32_t c = (w >> (8u * (j & 3u))) & 0xffu, dg = c - '0';
-          fr += 1u << kFrCountSh;
-          if (!(fr & kFrDigits) && (c == '+' || c == '-')) {
-            fr |= kFrDigits | (c == '-' ? kFrNeg : 0u);
-          } else if (dg < 10u) {
-            fr |= kFrDigits;
-            fv = fv * 10u + dg;
-          } else {
-            fr |= kFrStop;
-          }
-        }
+        const bool act = j < m && !(fr & kFrStop);
+        const uint32_t c = w0 & 0xffu, dg = c - '0';
+        w0 = __builtin_amdgcn_alignbyte(w1, w0, 1);
+        w1 = __builtin_amdgcn_alignbyte(w2, w1, 1);
+        w2 >>= 8;
+        const bool sign = !(fr & kFrDigits) && (c == '+' || c == '-');
+        const bool dig = dg < 10u;
+        const uint32_t flags = sign ? kFrDigits | (c == '-' ? kFrNeg : 0u) : dig ? kFrDigits : kFrStop;
+        fr = act ? (fr + (1u << kFrCountSh)) | flags : fr;
+        fv = act && !sign && dig ? fv * 10u + dg : fv;
       }
       if ((n > 12u && !(fr & kFrStop)) || ((fr >> kFrCountSh) & 0xffu) > kFrMaxValue) fr |= kFrDefer;
     }

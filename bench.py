@@ -62,7 +62,7 @@ CONFIGS = {
                  layout="dense_rm",
                  name="config3: 1M mixed 64 B-4 KiB Zipf requests, 0-32 headers (max_headers 32)"),
     "post": dict(gen=rhp.GEN_POST1K, seed=0x5EED0005, maxh=16, mode=rhp.MODE_HTTP, per_gpu=1 << 20,
-                 layout="compact",
+                 layout="dense",
                  name="config5: 1M x 1 KiB POST, Content-Length body skip, 5% malformed (http_read_request)"),
     # not a BASELINE config: the chunked body framing of http_read_request (http.c:73-160, 221-230),
     # SURVEY.md §8f row 3; the bodies are de-framed in place, so every launch starts from restored bytes

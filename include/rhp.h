@@ -265,6 +265,22 @@ typedef struct rhp_session_result {
 int rhp_fixup_sessions(const rhp_batch_t *batch, const rhp_session_t *sessions, uint32_t n_sessions,
                        rhp_session_result_t *results, uint64_t *req_start, void *stream);
 
+/* Dense copies of a parsed http batch's records (round 6: what the reactor
+ * copies back to the host, reactor/batch.c).  For each record slot i of a
+ * RHP_MODE_HTTP batch in RHP_LAYOUT_REQUEST_MAJOR (speculative or not), after
+ * the parse (and rhp_fixup_sessions, when used): the request record as
+ * rhp_req_dense_t dreq[i], the http record as rhp_http_compact_t hc[i] and the
+ * header lengths as u16 lens16[k * n + i], k < num_headers, in
+ * RHP_LAYOUT_DENSE's encodings (a record whose consumed follows from ret and
+ * body_len; a request whose http record is such a record and whose offsets
+ * follow the running sum with names of at most RHP_DENSE_NAME_MAX and values of
+ * at most RHP_DENSE_VALUE_MAX bytes -- a de-framed chunked body moves its
+ * request's bytes, so that request stays wide).
+ * Any other slot is marked RHP_HTTP_WIDE / RHP_DENSE_WIDE: its records are the
+ * batch's own.  Device pointers; launch status as rhp_parse_batch. */
+int rhp_pack_dense(const rhp_batch_t *batch, rhp_req_dense_t *dreq, rhp_http_compact_t *hc, uint16_t *lens16,
+                   void *stream);
+
 /* Which kernel implementation rhp_parse_batch uses (diagnostics / A-B tests). */
 enum rhp_impl {
   RHP_IMPL_DFA = 0,    /* lane-per-request byte DFA with LDS tables (default) */

@@ -38,6 +38,9 @@ int rhp_cpu_parse_batch(const rhp_batch_t *batch);
 int rhp_cpu_fixup_sessions(const rhp_batch_t *batch, const rhp_session_t *sessions, uint32_t n_sessions,
                            rhp_session_result_t *results, uint64_t *req_start);
 int rhp_emu_parse_batch(const rhp_batch_t *batch, uint64_t *stats);
+/* rhp_pack_dense (rhp.h) on the host, over host copies of the batch's records
+ * (the reactor's host-async parser exercises the dense copy-back with it) */
+int rhp_cpu_pack_dense(const rhp_batch_t *batch, rhp_req_dense_t *dreq, rhp_http_compact_t *hc, uint16_t *lens16);
 
 /* A parsed batch's header records as rhp_hdr_t, out[i * max_headers + k]
  * (request-major), from host copies of its reqs and hdrs in the batch's

@@ -65,10 +65,11 @@ SESSION_RESULT_DTYPE = np.dtype([("n_slots", "<u4"), ("more", "<u4"), ("consumed
 
 # exported C-ABI symbols of librhp.so, as declared in include/rhp.h
 RHP_SYMBOLS = ("rhp_parse_batch", "rhp_set_impl", "rhp_kernel_name", "rhp_version", "rhp_write_responses",
-               "rhp_fixup_sessions")
+               "rhp_fixup_sessions", "rhp_pack_dense")
 HOST_SYMBOLS = ("rhp_gen_size", "rhp_gen_fill", "rhp_gen_header_bytes", "rhp_splitmix64",
                 "rhp_emu_parse_batch", "rhp_cpu_parse_batch", "rhp_phr_parse_request", "rhp_http_read_cpu",
-                "rhp_cpu_fixup_sessions", "rhp_expand_records", "rhp_expand_http", "rhp_expand_reqs", "rhp_test_chunk_window",
+                "rhp_cpu_fixup_sessions", "rhp_expand_records", "rhp_expand_http", "rhp_expand_reqs", "rhp_cpu_pack_dense",
+                "rhp_test_chunk_window",
                 "rhp_test_chunk_exact")
 
 _rhp = None
@@ -148,6 +149,9 @@ def lib() -> ctypes.CDLL:
         _rhp.rhp_version.restype = ctypes.c_char_p
         _rhp.rhp_write_responses.argtypes = [ctypes.POINTER(RespBatch), ctypes.c_void_p]
         _rhp.rhp_write_responses.restype = ctypes.c_int
+        vp = ctypes.c_void_p
+        _rhp.rhp_pack_dense.argtypes = [ctypes.POINTER(Batch), vp, vp, vp, vp]
+        _rhp.rhp_pack_dense.restype = ctypes.c_int
     return _rhp
 
 
@@ -182,6 +186,8 @@ def host() -> ctypes.CDLL:
         _host.rhp_expand_records.restype = ctypes.c_int
         _host.rhp_expand_http.argtypes = [ctypes.POINTER(Batch), vp, vp, vp]
         _host.rhp_expand_reqs.argtypes = [ctypes.POINTER(Batch), vp, vp]
+        _host.rhp_cpu_pack_dense.argtypes = [ctypes.POINTER(Batch), vp, vp, vp]
+        _host.rhp_cpu_pack_dense.restype = ctypes.c_int
         _host.rhp_expand_reqs.restype = ctypes.c_int
         _host.rhp_expand_http.restype = ctypes.c_int
     return _host
@@ -515,6 +521,25 @@ def parse_batch(buf: np.ndarray, off: np.ndarray, max_headers: int = 16, mode: i
         return db.result()
     finally:
         lib().rhp_set_impl(IMPL_DFA)
+
+
+def pack_dense_cpu(res: Result, n: int, max_headers: int):
+    """rhp_cpu_pack_dense over the request-major http records of `res`: (dreq
+    u8[8n], hc u8[8n], lens16 u16[max_headers * n]) -- what rhp_pack_dense makes
+    on the device (include/rhp.h), the reactor's copy-back."""
+    reqs = np.ascontiguousarray(res.raw_reqs[: n * REQ_DTYPE.itemsize]) if res.raw_reqs is not None \
+        else np.ascontiguousarray(res.reqs).view(np.uint8)
+    hdrs = np.ascontiguousarray(res.raw_hdrs)
+    http = np.ascontiguousarray(res.raw_http)
+    b = Batch(None, None, None, 0, n, max_headers, MODE_HTTP, LAYOUT_REQUEST_MAJOR, _ptr(reqs), _ptr(hdrs),
+              _ptr(http), 0, 0, 0, None)
+    dreq = np.zeros(max(8 * n, 8), dtype=np.uint8)
+    hc = np.zeros(max(8 * n, 8), dtype=np.uint8)
+    lens = np.zeros(max(max_headers * n, 1), dtype=np.uint16)
+    rc = host().rhp_cpu_pack_dense(ctypes.byref(b), _ptr(dreq), _ptr(hc), _ptr(lens))
+    if rc != 0:
+        raise RuntimeError(f"rhp_cpu_pack_dense failed: {rc}")
+    return dreq[: 8 * n], hc[: 8 * n], lens[: max_headers * n]
 
 
 # ---------------------------------------------------------------------------

@@ -47,14 +47,27 @@ enum { PARSER_UNSET, PARSER_GPU, PARSER_HOST, PARSER_HOST_ASYNC };
 
 /* A slot's round lives in ONE buffer, the same layout on the host (pinned) and
  * the device: the input [bytes + RHP_PAD | offsets | sessions] goes over in one
- * H2D copy, the records and the (de-framed) bytes come back in one D2H copy:
- * [bytes | offsets | sessions | reqs | hdrs | http | req_start | session results] */
+ * H2D copy; then
+ * [bytes | offsets | sessions | reqs | hdrs | http | req_start | session results | dreq | hc | lens16]:
+ * the batch's own records (request-major, what rhp_fixup_sessions works on),
+ * the session results and, round 6, their dense copies (rhp_pack_dense:
+ * 8-byte request and http records, u16 header lengths header-major).  One D2H
+ * copy brings back the session results, the dense records and the length rows
+ * the round's requests use (the records had come back
+ * request-major at 176 B per request); a slot the dense form cannot hold (the
+ * exact path's irregular records, a de-framed chunked body) has the batch's own
+ * records fetched for the round, and the bytes come back only for chunked
+ * bodies (reactor_batch_result). */
 typedef struct slot
 {
   size_t       cap;          /* bytes of h_buf / d_buf */
   uint8_t     *h_buf, *d_buf;
   size_t       in_size, out_size;   /* this round: the input prefix, the whole layout */
-  size_t       o_off, o_sess, o_req, o_hdr, o_http, o_start, o_sres;
+  size_t       o_off, o_sess, o_req, o_hdr, o_http, o_start, o_sres, o_dreq, o_hc, o_lens;
+  rhp_req_dense_t    *h_dreq;
+  rhp_http_compact_t *h_hc;
+  uint16_t           *h_lens;
+  uint32_t            rows;   /* length rows the round's D2H copy brought back */
   uint8_t     *h_bytes;      /* = h_buf */
   uint64_t    *h_off;
   rhp_req_t   *h_req;
@@ -82,6 +95,8 @@ typedef struct batch_state
   slot_t       slot[REACTOR_BATCH_SLOTS];
   void        *d_work;
   int          diag_host;   /* RHP_REACTOR_DIAG=hostparse: gpu-mode buffers, host parse (diagnostic) */
+  int          pack;        /* gpu: the dense copy-back (RHP_REACTOR_PACK=0: the request-major records, A/B) */
+  uint32_t     rows_hint;   /* length rows the last round used: the next round's D2H copies as many */
   /* gpu: how a round's completion reaches the eventfd (RHP_REACTOR_COMPLETE):
    * COMPLETE_HOSTFUNC a hipLaunchHostFunc behind the round's copies (the HIP
    * runtime's callback thread writes the eventfd); COMPLETE_EVENT a waiter
@@ -284,6 +299,11 @@ static int parser(void)
     B->delay_us = dl ? atoi(dl) : 0;
     const char *dg = getenv("RHP_REACTOR_DIAG");
     B->diag_host = dg && strcmp(dg, "hostparse") == 0;
+    /* the dense copy-back: gpu and host-async (the gpu protocol on the CPU) by
+     * default, RHP_REACTOR_PACK=0 / 1 to choose */
+    const char *pk = getenv("RHP_REACTOR_PACK");
+    B->pack = pk ? strcmp(pk, "0") != 0 : B->parser != PARSER_HOST;
+    B->rows_hint = 4;
     B->efd = -1;
     if (B->parser == PARSER_GPU)
     {
@@ -386,7 +406,10 @@ uint8_t *reactor_batch_reserve(int k, size_t bytes, uint32_t n, uint32_t n_sessi
   s->o_http = s->o_hdr + up16((size_t) n * REACTOR_BATCH_HEADERS * sizeof(rhp_hdr_t));
   s->o_start = s->o_http + up16(n * sizeof(rhp_http_t));
   s->o_sres = s->o_start + up16(n * sizeof(uint64_t));
-  s->out_size = s->o_sres + up16(n_sessions * sizeof(rhp_session_result_t));
+  s->o_dreq = s->o_sres + up16(n_sessions * sizeof(rhp_session_result_t));
+  s->o_hc = s->o_dreq + up16(n * sizeof(rhp_req_dense_t));
+  s->o_lens = s->o_hc + up16(n * sizeof(rhp_http_compact_t));
+  s->out_size = s->o_lens + up16((size_t) n * REACTOR_BATCH_HEADERS * sizeof(uint16_t));
   if (s->out_size > s->cap)
   {
     /* generous first capacities: growing pinned and device buffers costs
@@ -416,6 +439,9 @@ uint8_t *reactor_batch_reserve(int k, size_t bytes, uint32_t n, uint32_t n_sessi
   s->h_http = (rhp_http_t *) (s->h_buf + s->o_http);
   s->h_start = (uint64_t *) (s->h_buf + s->o_start);
   s->h_sres = (rhp_session_result_t *) (s->h_buf + s->o_sres);
+  s->h_dreq = (rhp_req_dense_t *) (s->h_buf + s->o_dreq);
+  s->h_hc = (rhp_http_compact_t *) (s->h_buf + s->o_hc);
+  s->h_lens = (uint16_t *) (s->h_buf + s->o_lens);
   return s->h_bytes;
 }
 
@@ -447,6 +473,8 @@ static void host_parse(batch_state_t *st, int k)
     .flags = RHP_BATCH_SPECULATIVE};
   (void) rhp_cpu_parse_batch(&b);
   (void) rhp_cpu_fixup_sessions(&b, s->h_sess, s->n_sess, s->h_sres, s->h_start);
+  if (st->pack)   /* the gpu mode's dense records (host-async: its copy-back protocol on the CPU) */
+    (void) rhp_cpu_pack_dense(&b, s->h_dreq, s->h_hc, s->h_lens);
 }
 
 void reactor_batch_submit(int k, uint32_t n, size_t bytes, uint32_t n_sessions)
@@ -519,10 +547,23 @@ void reactor_batch_submit(int k, uint32_t n, size_t bytes, uint32_t n_sessions)
     HIP(hipEventRecord(s->tev[3], B->stream));
     s->t_launch_calls = now_ns() - t_l0;
   }
-  /* the records: one asynchronous copy of the layout's output part (the
-   * bytes, de-framed in place where a body is chunked, http.c:155, come back
-   * only for a round that has such a body: reactor_batch_result) */
-  HIP(hipMemcpyAsync(s->h_buf + s->o_req, s->d_buf + s->o_req, s->out_size - s->o_req, hipMemcpyDeviceToHost, B->stream));
+  /* the records: one asynchronous copy (the bytes, de-framed in place where a
+   * body is chunked, http.c:155, come back only for a round that has such a
+   * body: reactor_batch_result).  Dense (B->pack): the session results, the
+   * 8-byte request and http records and as many u16 length rows as the last
+   * round used; the request-major records otherwise. */
+  if (B->pack)
+  {
+    rc = rhp_pack_dense(&b, (rhp_req_dense_t *) (d + s->o_dreq), (rhp_http_compact_t *) (d + s->o_hc),
+                        (uint16_t *) (d + s->o_lens), B->stream);
+    if (rc != 0)
+      die("rhp_pack_dense", rc);
+    s->rows = B->rows_hint < REACTOR_BATCH_HEADERS ? B->rows_hint : REACTOR_BATCH_HEADERS;
+    const size_t end = s->o_lens + (size_t) s->rows * n * sizeof(uint16_t);
+    HIP(hipMemcpyAsync(s->h_buf + s->o_sres, s->d_buf + s->o_sres, end - s->o_sres, hipMemcpyDeviceToHost, B->stream));
+  }
+  else
+    HIP(hipMemcpyAsync(s->h_buf + s->o_req, s->d_buf + s->o_req, s->o_dreq - s->o_req, hipMemcpyDeviceToHost, B->stream));
   if (tl)
   {
     HIP(hipEventRecord(s->tev[4], B->stream));
@@ -586,7 +627,44 @@ void reactor_batch_result(int k, reactor_batch_result_t *out)
       s->t_wake = 0;
     }
   }
-  if (B->parser == PARSER_GPU && !B->diag_host)
+  bool wide = !B->pack || (B->parser == PARSER_GPU && B->diag_host);   /* the request-major records are on the host */
+  if (!wide)
+  {
+    /* the dense copy-back (reactor_batch_submit): the length rows the owned
+     * slots' dense requests use beyond the ones copied, and the batch's own
+     * records when some owned slot is wide (the exact path's, a de-framed
+     * chunked body); the next round copies as many rows as this one used */
+    uint32_t rows = 0;
+    for (uint32_t q = 0; q < s->n_sess; q++)
+      for (uint32_t i = s->h_sess[q].piece_lo; i < s->h_sess[q].piece_lo + s->h_sres[q].n_slots && i < s->n; i++)
+      {
+        /* a wide http record's request is wide too (rhp_pack_dense) */
+        const bool hw = s->h_hc[i].flags & RHP_HTTP_WIDE;
+        const bool rw = !hw && s->h_hc[i].result == 1 && (s->h_dreq[i].flags & RHP_DENSE_WIDE);
+        wide |= hw || rw;
+        if (!hw && s->h_hc[i].result == 1 && !rw && s->h_dreq[i].num_headers > rows)
+          rows = s->h_dreq[i].num_headers;
+      }
+    bool sync = false;
+    const bool dev = B->parser == PARSER_GPU;   /* host-async: every record is on the host already */
+    if (dev && !B->cstream)
+      HIP(hipStreamCreateWithFlags(&B->cstream, hipStreamNonBlocking));
+    if (dev && rows > s->rows)
+    {
+      const size_t a = s->o_lens + (size_t) s->rows * s->n * sizeof(uint16_t), e = s->o_lens + (size_t) rows * s->n * sizeof(uint16_t);
+      HIP(hipMemcpyAsync(s->h_buf + a, s->d_buf + a, e - a, hipMemcpyDeviceToHost, B->cstream));
+      sync = true;
+    }
+    if (dev && wide)
+    {
+      HIP(hipMemcpyAsync(s->h_buf + s->o_req, s->d_buf + s->o_req, s->o_sres - s->o_req, hipMemcpyDeviceToHost, B->cstream));
+      sync = true;
+    }
+    if (sync)
+      HIP(hipStreamSynchronize(B->cstream));
+    B->rows_hint = rows ? rows : 1;
+  }
+  if (B->parser == PARSER_GPU && !B->diag_host && wide)
   {
     /* only the records came back (reactor_batch_submit): the bytes, de-framed
      * in place by the fix-up, are fetched when some request of the round has a
@@ -649,6 +727,59 @@ void reactor_batch_result(int k, reactor_batch_result_t *out)
   out->session_results = s->h_sres;
   out->req_start = s->h_start;
   out->n_sessions = s->n_sess;
+  out->dense = B->pack && !(B->parser == PARSER_GPU && B->diag_host);
+  out->dreq = s->h_dreq;
+  out->hc = s->h_hc;
+  out->lens16 = s->h_lens;
+}
+
+void reactor_batch_record(const reactor_batch_result_t *r, uint32_t i, rhp_req_t *req, rhp_http_t *x, rhp_hdr_t *h,
+                          const rhp_hdr_t **hp)
+{
+  if (!r->dense)
+  {
+    *req = r->reqs[i];
+    *x = r->http[i];
+    *hp = r->hdrs + (size_t) i * REACTOR_BATCH_HEADERS;
+    return;
+  }
+  const rhp_http_compact_t c = r->hc[i];
+  const rhp_req_dense_t d = r->dreq[i];
+  const int result = c.flags & RHP_HTTP_WIDE ? r->http[i].result : c.result;
+  const bool rw = result == 1 && (d.flags & RHP_DENSE_WIDE);
+  if (rw)
+  {
+    *req = r->reqs[i];
+    *hp = r->hdrs + (size_t) i * REACTOR_BATCH_HEADERS;
+  }
+  else
+  {
+    /* rhp.h dense records: path_off = method_len + 1, the header offsets a running sum */
+    memset(req, 0, sizeof *req);
+    req->ret = d.ret;
+    req->method_len = d.method_len;
+    req->path_off = (uint16_t) (d.method_len + 1u);
+    req->path_len = d.path_len;
+    req->minor_version = (int8_t) d.minor_version;
+    req->num_headers = d.num_headers;
+    uint32_t at = (uint32_t) req->path_off + req->path_len + 11u;
+    for (uint32_t k = 0; k < d.num_headers && result == 1; k++)
+    {
+      const uint32_t l = r->lens16[(size_t) k * r->n + i], nl = l & 63u, vl = l >> 6;
+      h[k] = (rhp_hdr_t) {(uint16_t) at, (uint16_t) nl, (uint16_t) (at + nl + 2u), (uint16_t) vl};
+      at += nl + vl + 4u;
+    }
+    *hp = h;
+  }
+  if (c.flags & RHP_HTTP_WIDE)
+    *x = r->http[i];
+  else
+  {
+    x->result = c.result;
+    x->body_kind = c.body_kind;
+    x->body_len = c.body_len;
+    x->consumed = c.result == 1 ? (uint64_t) (uint32_t) req->ret + (c.body_kind == 1 ? c.body_len : 0u) : 0u;
+  }
 }
 
 enum { WRITER_HOST, WRITER_HOST_BATCH, WRITER_GPU };

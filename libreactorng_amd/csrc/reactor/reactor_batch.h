@@ -24,7 +24,20 @@ typedef struct reactor_batch_result
   const rhp_session_result_t *session_results;
   const uint64_t             *req_start;
   uint32_t                    n_sessions;
+  /* gpu (round 6): the dense copies the round brought back (rhp_pack_dense);
+   * reqs / hdrs / http / req_start are then valid only for slots marked wide.
+   * Read a slot through reactor_batch_record. */
+  int                         dense;
+  const rhp_req_dense_t      *dreq;
+  const rhp_http_compact_t   *hc;
+  const uint16_t             *lens16;   /* header-major, n per row */
 } reactor_batch_result_t;
+
+/* record slot i of a result: its request, http and header records (expanded
+ * from the dense copies into *req, *x and h[REACTOR_BATCH_HEADERS], or the
+ * batch's own; *hp is the header records, one per request header, stride 1) */
+void reactor_batch_record(const reactor_batch_result_t *r, uint32_t i, rhp_req_t *req, rhp_http_t *x, rhp_hdr_t *h,
+                          const rhp_hdr_t **hp);
 
 /* 1: rounds complete asynchronously (gpu parser) and each completion adds 1 to
  * the eventfd reactor_batch_fd(); 0: reactor_batch_submit parses in place */

@@ -335,7 +335,12 @@ static bool server_session_dispatch(server_session_t *s, uint32_t lo, const rhp_
       break;
     }
     const uint32_t i = lo + m;
-    const rhp_http_t *x = &res->http[i];
+    rhp_req_t rq;
+    rhp_http_t hx;
+    rhp_hdr_t hbuf[REACTOR_BATCH_HEADERS];
+    const rhp_hdr_t *hp;
+    reactor_batch_record(res, i, &rq, &hx, hbuf, &hp);
+    const rhp_http_t *x = &hx;
     int result = x->result;
     size_t consumed = 0;
     if (result == RHP_RET_TOOLONG)
@@ -361,9 +366,9 @@ static bool server_session_dispatch(server_session_t *s, uint32_t lo, const rhp_
     if (x->result != RHP_RET_TOOLONG)
     {
       uint8_t *base = data_base(in);
-      if (x->body_kind && x->consumed != (uint64_t) res->reqs[i].ret + x->body_len)
+      if (x->body_kind && x->consumed != (uint64_t) rq.ret + x->body_len)
         memcpy(base, res->bytes + res->req_start[i], x->consumed);   /* chunked body, de-framed in place */
-      reactor_http_fill(base, &res->reqs[i], res->hdrs + (size_t) i * REACTOR_BATCH_HEADERS, 1, x,
+      reactor_http_fill(base, &rq, hp, 1, x,
                         &s->request.method, &s->request.target, &s->request.body, s->request.fields,
                         &s->request.fields_count);
       consumed = x->consumed;

@@ -460,6 +460,37 @@ extern "C" int rhp_expand_http(const rhp_batch_t *b, const rhp_req_t *reqs, cons
   return 0;
 }
 
+/* rhp_pack_dense (rhp.h) on the host: the same encodings as the kernel's
+ * (rhp_kernel.hip rhp_pack_dense_kernel), for the reactor's host-async parser */
+extern "C" int rhp_cpu_pack_dense(const rhp_batch_t *b, rhp_req_dense_t *dreq, rhp_http_compact_t *hc, uint16_t *lens16)
+{
+  if (!b || b->mode != RHP_MODE_HTTP || b->layout != RHP_LAYOUT_REQUEST_MAJOR || b->max_headers > RHP_MAX_HEADERS) return -22;
+  const uint32_t n = b->n, m = b->max_headers;
+  for (uint32_t i = 0; i < n; i++) {
+    const rhp_req_t r = b->reqs[i];
+    const rhp_http_t x = b->http[i];
+    const uint64_t cons = x.result == 1 ? (uint64_t) (uint32_t) r.ret + (x.body_kind == 1 ? x.body_len : 0u) : 0u;
+    const bool hok = x.consumed == cons && x.body_kind <= 1u && !(x.body_len >> 32) && (x.result != 1 || r.ret > 0);
+    hc[i] = hok ? rhp_http_compact_t{(int8_t) x.result, (uint8_t) x.body_kind, 0, 0, (uint32_t) x.body_len}
+                : rhp_http_compact_t{0, 0, (uint8_t) RHP_HTTP_WIDE, 0, 0};
+    bool reg = hok && x.result == 1 && r.ret > 0 && r.ret <= (int32_t) RHP_MAX_LEN && r.method_off == 0 && r.method_len <= 255u &&
+               r.path_off == r.method_len + 1u && r.num_headers <= m;
+    uint32_t at = (uint32_t) r.path_off + r.path_len + 11u;
+    const uint32_t nh = reg ? r.num_headers : 0u;
+    for (uint32_t k = 0; k < nh; k++) {
+      const rhp_hdr_t h = b->hdrs[(uint64_t) i * m + k];
+      reg = reg && h.name_off == at && h.value_off == at + h.name_len + 2u &&
+            std::max((uint32_t) h.name_len << 4, (uint32_t) h.value_len) <= RHP_DENSE_VALUE_MAX;
+      at += (uint32_t) h.name_len + h.value_len + 4u;
+      lens16[(uint64_t) k * n + i] = (uint16_t) (h.name_len | (uint32_t) h.value_len << 6);
+    }
+    dreq[i] = reg ? rhp_req_dense_t{(uint16_t) r.ret, r.path_len, (uint8_t) r.method_len, (uint8_t) r.num_headers,
+                                    (uint8_t) r.minor_version, 0}
+                  : rhp_req_dense_t{0, 0, 0, 0, 0, (uint8_t) RHP_DENSE_WIDE};
+  }
+  return 0;
+}
+
 /* rhp_fixup_sessions (rhp.h) on the host: the same walk (rhp_scalar.h
  * fixup_session_t) over a speculative batch parsed by rhp_cpu_parse_batch or
  * rhp_emu_parse_batch. */

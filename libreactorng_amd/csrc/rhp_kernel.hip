@@ -1465,7 +1465,16 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * 16-byte parts hold whole dwords): a fresh candidate's name (compared
    * with both names) and its value from r + 16 (the one SP after the colon),
    * or the continuation of a Content-Length value from r. */
-  auto frame_window = [&](uint32_t crec_before) __attribute__((always_inline)) {
+  /* frame_read: which bytes the lane needs and their LDS reads (issued; the
+   * caller waits for them); frame_eval: the rest.  Split so that the next
+   * window's issue, which refills the staging buffer, can go out between the
+   * two (RHP_FRAME_SPLIT) */
+  struct FrameIn {
+    bool need, fresh, rec_done;
+    uint32_t r, n, nl, value_len;
+    uint32_t raw[10];
+  };
+  auto frame_read = [&](FrameIn &fi, uint32_t crec_before) __attribute__((always_inline)) {
     const uint32_t wend = (uint32_t) dpos + kWBlock;
     const uint32_t hdr = cand & 0x3fffffffu;
     const bool rec_done = (crec_lo | (cand & 0xbfffffffu)) != crec_before && hdr != 0 && (hdr & (hdr - 1u)) == 0 &&
@@ -1502,18 +1511,32 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         }
       }
     }
+    fi.need = need;
+    fi.fresh = fresh;
+    fi.rec_done = rec_done;
+    fi.r = r;
+    fi.n = n;
+    fi.nl = nl;
+    fi.value_len = value_len;
     if (!__builtin_amdgcn_ballot_w64(need)) return;
     if (!need) return;
-    uint32_t raw[10], d[9];
-    const uint32_t b0 = (r - (uint32_t) dpos) & ~3u, sh = (r - (uint32_t) dpos) & 3u;
+    const uint32_t b0 = (r - (uint32_t) dpos) & ~3u;
 #pragma unroll
     for (uint32_t k = 0; k < 10; k++) {   /* bytes past the window wrap inside the lane's window: never used */
       const uint32_t b = b0 + 4u * k;
-      raw[k] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(
+      fi.raw[k] = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(
           (size_t) (part_lds((b >> 4) % kWParts) + (b & 15u)));
     }
+  };
+  auto frame_eval = [&](FrameIn &fi) __attribute__((always_inline)) {
+    if (!__builtin_amdgcn_ballot_w64(fi.need)) return;
+    if (!fi.need) return;
+    const bool fresh = fi.fresh, rec_done = fi.rec_done;
+    const uint32_t r = fi.r, n = fi.n, nl = fi.nl, value_len = fi.value_len;
+    uint32_t d[9];
+    const uint32_t sh = (r - (uint32_t) dpos) & 3u;
 #pragma unroll
-    for (uint32_t k = 0; k < 9; k++) d[k] = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh);
+    for (uint32_t k = 0; k < 9; k++) d[k] = __builtin_amdgcn_alignbyte(fi.raw[k + 1], fi.raw[k], sh);
     bool digits = !fresh;
     if (fresh) {
       /* case-insensitive compares (OR 0x20: the one non-letter, '-', could
@@ -1578,6 +1601,11 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       }
       if ((n > 12u && !(fr & kFrStop)) || ((fr >> kFrCountSh) & 0xffu) > kFrMaxValue) fr |= kFrDefer;
     }
+  };
+  auto frame_window = [&](uint32_t crec_before) __attribute__((always_inline)) {
+    FrameIn fi;
+    frame_read(fi, crec_before);
+    frame_eval(fi);
   };
   /* set up the decode of the window walked last iteration */
   auto decode_begin = [&]() {
@@ -2110,6 +2138,33 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (any_walk) decode_window();
 #endif
       dg.section(kSecDecodeStamp, true);
+#ifdef RHP_FRAME_SPLIT
+      /* the framing's reads of the staging buffer, the next window's issue,
+       * then the framing's evaluation and the finalize (which the issue does
+       * not wait for: a walk ends at a terminal, its last byte or a max_headers
+       * stop, all known after the decode) */
+      FrameIn fi;
+      fi.need = false;
+#ifndef RHP_DIAG_NO_FRAME
+      if (http && any_walk) frame_read(fi, crec_before);
+#endif
+      if (walking && (ovf != 0 || is_done2(st) || is_err2(st) || is_slow2(st) ||
+                      (uint32_t) (wpos + (int32_t) kWBlock) >= wlen))
+        wact = false;
+      nw = 0;
+      if (walking && wact) nw = (cur_ptr + kWBlock) | 1u;
+      else if (pend_ok && (!kPhaseLock || it_odd)) nw = first_win(pend_o0) | 2u;   /* the next iteration is even */
+      Issue is;
+      issue_prep(is);   /* the address shuffles go out with the framing's reads */
+      wait_lgkm0();     /* the framing's reads of the buffer are done */
+      issue_go(is);
+#ifndef RHP_DIAG_NO_FRAME
+      if (http && any_walk) frame_eval(fi);
+#endif
+      dg.section(kSecFrameStamp, true);
+      if (any_walk) (void) decode_end();
+      dg.section(2, true);
+#else
 #ifndef RHP_DIAG_NO_FRAME   /* diagnostic builds only: the in-loop framing's share */
       if (http && any_walk) frame_window(crec_before);
 #endif
@@ -2127,6 +2182,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       else if (pend_ok && (!kPhaseLock || it_odd)) nw = first_win(pend_o0) | 2u;   /* the next iteration is even */
       wait_lgkm0();   /* the decode's reads of the buffer are done */
       issue();
+#endif
     }
     dg.section(LATE ? 4 : 3, true);
     /* [G] */
@@ -2388,6 +2444,39 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
   dg.exit(WAVES);
 }
 
+/* rhp_pack_dense (rhp.h): one thread per record slot, the dense encodings of
+ * its request-major records (the host expands them: reactor/batch.c) */
+__global__ __launch_bounds__(256) void rhp_pack_dense_kernel(const rhp_req_t *reqs, const rhp_hdr_t *hdrs,
+                                                             const rhp_http_t *http, uint32_t n, uint32_t m, uint2 *dreq,
+                                                             uint2 *hc, uint16_t *lens16)
+{
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const rhp_req_t r = reqs[i];
+  const rhp_http_t x = http[i];
+  /* the http record: compact when its consumed follows from ret (rhp.h) */
+  const uint64_t cons = x.result == 1 ? (uint64_t) (uint32_t) r.ret + (x.body_kind == 1 ? x.body_len : 0u) : 0u;
+  const bool hok = x.consumed == cons && x.body_kind <= 1u && !(x.body_len >> 32) && (x.result != 1 || r.ret > 0);
+  hc[i] = hok ? uint2{((uint32_t) x.result & 0xffu) | x.body_kind << 8, (uint32_t) x.body_len} : uint2{RHP_HTTP_WIDE << 16, 0u};
+  /* the request: dense when the DFA's regular form holds it and the http
+   * record is compact (a de-framed chunked body moves its request's bytes:
+   * the wide records' offsets are the moved ones) */
+  bool reg = hok && x.result == 1 && r.ret > 0 && r.ret <= (int32_t) RHP_MAX_LEN && r.method_off == 0 && r.method_len <= 255u &&
+             r.path_off == r.method_len + 1u && r.num_headers <= m;
+  uint32_t at = (uint32_t) r.path_off + r.path_len + 11u;
+  const uint32_t nh = reg ? r.num_headers : 0u;
+  for (uint32_t k = 0; k < nh; k++) {
+    const rhp_hdr_t h = hdrs[(uint64_t) i * m + k];
+    reg = reg && h.name_off == at && h.value_off == at + h.name_len + 2u &&
+          max((uint32_t) h.name_len << 4, (uint32_t) h.value_len) <= RHP_DENSE_VALUE_MAX;
+    at += (uint32_t) h.name_len + h.value_len + 4u;
+    lens16[(uint64_t) k * n + i] = (uint16_t) (h.name_len | (uint32_t) h.value_len << 6);
+  }
+  dreq[i] = reg ? uint2{(uint32_t) r.ret | (uint32_t) r.path_len << 16,
+                        r.method_len | (uint32_t) r.num_headers << 8 | ((uint32_t) (uint8_t) r.minor_version) << 16}
+                : uint2{0u, RHP_DENSE_WIDE << 24};
+}
+
 /* rhp_fixup_sessions: one wave per session.  The wave first takes the
  * session's leading pieces whose speculative record is the whole piece -- a
  * request that ended exactly at the piece's end with no chunked body to
@@ -2616,6 +2705,17 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
   if (compact) return late ? launch_dfa<16, true, false, kRecCompact>(prm, s, dev, cus) : launch_dfa<16, false, false, kRecCompact>(prm, s, dev, cus);
   if (late) return launch_dfa<16, true, false, kRecWide>(prm, s, dev, cus);
   return launch_dfa<16, false, false, kRecWide>(prm, s, dev, cus);
+}
+
+int rhp_pack_dense(const rhp_batch_t *b, rhp_req_dense_t *dreq, rhp_http_compact_t *hc, uint16_t *lens16, void *stream)
+{
+  if (!b || (b->n && (!b->reqs || !b->http || !dreq || !hc || (b->max_headers && (!b->hdrs || !lens16))))) return -22;
+  if (b->mode != RHP_MODE_HTTP || b->layout != RHP_LAYOUT_REQUEST_MAJOR || b->max_headers > RHP_MAX_HEADERS) return -22;
+  if (b->n == 0) return 0;
+  hipLaunchKernelGGL(rhp_pack_dense_kernel, dim3((b->n + 255u) / 256u), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     b->reqs, b->hdrs, b->http, b->n, b->max_headers, reinterpret_cast<uint2 *>(dreq),
+                     reinterpret_cast<uint2 *>(hc), lens16);
+  return (int) hipGetLastError();
 }
 
 int rhp_fixup_sessions(const rhp_batch_t *b, const rhp_session_t *sessions, uint32_t n_sessions,

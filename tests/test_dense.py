@@ -231,3 +231,105 @@ def test_gpu_dense_http_full_size_matches_reference_digest(name):
         raise AssertionError(f"{name}: dense digest differs from the reference but matches the oracle")
     if "bytes_out_sha256" in spec:
         assert hashlib.sha256(res.bytes_out.tobytes()).hexdigest() == spec["bytes_out_sha256"]
+
+
+# ---------------------------------------------------------------------------
+# rhp_pack_dense (include/rhp.h): the dense copies of a request-major http
+# batch's records, what the reactor copies back (reactor/batch.c)
+
+def check_pack(res, n, maxh):
+    """the packed copies of `res` (rhp_cpu_pack_dense) rebuild its records where
+    they claim to; returns how many requests were dense"""
+    dreq, hc, lens = rhp.pack_dense_cpu(res, n, maxh)
+    d = dreq.reshape(n, 8)
+    c = hc.reshape(n, 8)
+    lens = lens.reshape(maxh, n) if maxh else lens[:0].reshape(0, n)
+    dense = 0
+    for i in range(n):
+        r, x = res.reqs[i], res.http[i]
+        cons = int(r["ret"]) + (int(x["body_len"]) if x["body_kind"] == 1 else 0) if x["result"] == 1 else 0
+        compact = (int(x["consumed"]) == cons and x["body_kind"] <= 1 and int(x["body_len"]) < 1 << 32
+                   and (x["result"] != 1 or r["ret"] > 0))
+        if c[i, 2] & rhp.HTTP_WIDE:
+            assert not compact, i
+        else:
+            assert compact, i
+            assert int(np.int8(c[i, 0])) == x["result"] and c[i, 1] == x["body_kind"], i
+            assert int(c[i, 4:8].view(np.uint32)[0]) == x["body_len"], i
+        if d[i, 7] & rhp.DENSE_WIDE:
+            continue
+        dense += 1
+        assert compact and x["result"] == 1, i
+        ret, plen = int(d[i, 0:2].view(np.uint16)[0]), int(d[i, 2:4].view(np.uint16)[0])
+        assert (ret, plen, d[i, 4], d[i, 5], d[i, 6]) == (r["ret"], r["path_len"], r["method_len"],
+                                                         r["num_headers"], r["minor_version"]), i
+        assert r["method_off"] == 0 and r["path_off"] == r["method_len"] + 1, i
+        at = int(r["path_off"]) + plen + 11
+        for k in range(int(d[i, 5])):
+            h = res.hdrs[i, k]
+            nl, vl = int(lens[k, i]) & 63, int(lens[k, i]) >> 6
+            assert (h["name_off"], h["name_len"], h["value_off"], h["value_len"]) == (at, nl, at + nl + 2, vl), (i, k)
+            at += nl + vl + 4
+    return dense
+
+
+@pytest.mark.parametrize("name", HTTP_SETS)
+def test_pack_dense_cpu_rebuilds_records(name):
+    spec, buf, off, _ = golden(name)
+    n, maxh = len(off) - 1, spec["max_headers"]
+    res = rhp.parse_cpu_exact(buf, off, maxh, rhp.MODE_HTTP)
+    dense = check_pack(res, n, maxh)
+    assert dense > 0 or "chunked" in name   # (every chunked body de-framed: all wide)
+
+
+def test_pack_dense_cpu_fixup_chunked_stays_wide():
+    """a chunked body de-framed by the fix-up moves its request's bytes: its
+    request and http records stay wide"""
+    streams = [b"GET /a HTTP/1.1\r\nHost: x\r\n\r\n"
+               b"POST /c HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n5\r\nhello\r\n6\r\n world\r\n0\r\n\r\n"
+               b"POST /l HTTP/1.1\r\nContent-Length: 3\r\n\r\nabcGET /z HTTP/1.0\r\n\r\n"]
+    buf, off, sess, _ = rhp.pack_sessions(streams)
+    res, sres, _ = rhp.fixup_cpu(buf, off, sess, 16)
+    n = len(off) - 1
+    dreq, hc, _ = rhp.pack_dense_cpu(res, n, 16)
+    check_pack(res, n, 16)
+    slots = range(int(sess[0]["piece_lo"]), int(sess[0]["piece_lo"]) + int(sres[0]["n_slots"]))
+    kinds = [(int(res.http[i]["body_kind"]), bool(dreq[8 * i + 7] & rhp.DENSE_WIDE),
+              bool(hc[8 * i + 2] & rhp.HTTP_WIDE)) for i in slots]
+    assert kinds == [(0, False, False), (1, True, True), (1, False, False), (0, False, False)], kinds
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["golden", "post", "chunked", "fuzz"])
+def test_gpu_pack_dense_equals_cpu_pack(case):
+    """rhp_pack_dense on the device's records, byte for byte the CPU pack of
+    the same records (their parity with the oracle is the other tests')"""
+    import ctypes
+    import torch
+    if case == "golden":
+        spec, buf, off, _ = golden(HTTP_SETS[0])
+        maxh = spec["max_headers"]
+    else:
+        gen = {"post": rhp.GEN_POST1K, "chunked": rhp.GEN_CHUNKED, "fuzz": rhp.GEN_FUZZ_HTTP}[case]
+        buf, off = rhp.generate(gen, 20000, 77, lo=1000 if case != "fuzz" else 0)
+        maxh = 16
+    n = len(off) - 1
+    db = rhp.DeviceBatch(buf, off, maxh, rhp.MODE_HTTP, layout=rhp.LAYOUT_REQUEST_MAJOR)
+    db.launch()
+    dd = torch.zeros(8 * n, dtype=torch.uint8, device="cuda")
+    dh = torch.zeros(8 * n, dtype=torch.uint8, device="cuda")
+    dl = torch.zeros(max(maxh * n, 1), dtype=torch.int16, device="cuda")
+    d = db.desc()
+    rc = rhp.lib().rhp_pack_dense(ctypes.byref(d), dd.data_ptr(), dh.data_ptr(), dl.data_ptr(),
+                                  torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    res = db.result()
+    want_d, want_h, want_l = rhp.pack_dense_cpu(res, n, maxh)
+    got_l = dl.cpu().numpy().view(np.uint16)[: maxh * n]
+    assert (dd.cpu().numpy() == want_d).all()
+    assert (dh.cpu().numpy() == want_h).all()
+    # rows past a request's num_headers are unspecified: compare the used ones
+    nh = np.where((want_d.reshape(n, 8)[:, 7] & rhp.DENSE_WIDE) == 0, want_d.reshape(n, 8)[:, 5], 0)
+    used = np.arange(maxh)[:, None] < nh[None, :]
+    assert (got_l.reshape(maxh, n)[used] == want_l.reshape(maxh, n)[used]).all()
+    assert check_pack(res, n, maxh) > 0

@@ -8,6 +8,7 @@
 #   lines  tools/ubench_lines (window line order vs bandwidth; built beforehand)
 #   ab     tools/ab_libs.py over AB_LIBS ("tag=path ...") for each of AB_CONFIGS
 #   stamps tools/stamps2.py on the RHP_STAMPS build (librhp_x_stamps.so) for STAMPS_CFG
+#   reactor tools/reactor_timeline.sh and two tools/reactor_crossover.py runs
 # (round 6: one script for every session; the per-session env is recorded in
 # the profiles README that keeps its output)
 set -o pipefail
@@ -75,11 +76,18 @@ step_stamps() {
   RHP_LIB=$PWD/libreactorng_amd/librhp_x_stamps.so timeout -k 10 300 python3 tools/stamps2.py > gpurun_out/stamps_${TAG}.txt 2>&1 \
     && grep -v Warning gpurun_out/stamps_${TAG}.txt | head -40
 }
+step_reactor() {
+  timeout -k 10 400 bash tools/reactor_timeline.sh > gpurun_out/reactor_timeline_${TAG}.txt 2>&1 \
+    && timeout -k 10 400 python3 tools/reactor_crossover.py > gpurun_out/reactor_crossover_${TAG}_1.txt 2>&1 \
+    && timeout -k 10 400 python3 tools/reactor_crossover.py > gpurun_out/reactor_crossover_${TAG}_2.txt 2>&1 \
+    && cat gpurun_out/reactor_crossover_${TAG}_1.txt gpurun_out/reactor_crossover_${TAG}_2.txt
+}
 step_smoke() {
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" > gpurun_out/smoke_${TAG}.log 2>&1 \
     && tail -1 gpurun_out/smoke_${TAG}.log
 }
 ( ! has quick || step_quick ) && ( ! has lines || step_lines ) && ( ! has ab || step_ab ) && ( ! has stamps || step_stamps ) \
+  && ( ! has reactor || step_reactor ) \
   && ( ! has tests || step_tests ) && ( ! has bench || step_bench ) && ( ! has prof || step_prof ) && ( ! has pmc || step_pmc ) \
   && ( ! has sq || step_sq ) && ( ! has writer || step_writer ) && ( ! has smoke || step_smoke ) \
   && ( ! has ceil || step_ceil ) && echo SESSION_OK

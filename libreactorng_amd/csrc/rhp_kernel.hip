@@ -1467,8 +1467,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * or the continuation of a Content-Length value from r. */
   /* frame_read: which bytes the lane needs and their LDS reads (issued; the
    * caller waits for them); frame_eval: the rest.  Split so that the next
-   * window's issue, which refills the staging buffer, can go out between the
-   * two (RHP_FRAME_SPLIT) */
+   * window's issue, which refills the staging buffer, goes out between the
+   * two */
   struct FrameIn {
     bool need, fresh, rec_done;
     uint32_t r, n, nl, value_len;
@@ -2138,11 +2138,14 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if (any_walk) decode_window();
 #endif
       dg.section(kSecDecodeStamp, true);
-#ifdef RHP_FRAME_SPLIT
+#ifndef RHP_FRAME_JOINED
       /* the framing's reads of the staging buffer, the next window's issue,
        * then the framing's evaluation and the finalize (which the issue does
        * not wait for: a walk ends at a terminal, its last byte or a max_headers
-       * stop, all known after the decode) */
+       * stop, all known after the decode): the window has the evaluation and
+       * the finalize to land in (config 5 78.4 -> 75.1 us same-box,
+       * profiles/r06/ab/ab_r6m_post.txt; RHP_FRAME_JOINED: the issue after
+       * the finalize, as before) */
       FrameIn fi;
       fi.need = false;
 #ifndef RHP_DIAG_NO_FRAME

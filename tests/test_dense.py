@@ -307,7 +307,7 @@ def test_gpu_pack_dense_equals_cpu_pack(case):
     import ctypes
     import torch
     if case == "golden":
-        spec, buf, off, _ = golden(HTTP_SETS[0])
+        spec, buf, off, _ = golden([s for s in HTTP_SETS if "chunked" not in s][0])
         maxh = spec["max_headers"]
     else:
         gen = {"post": rhp.GEN_POST1K, "chunked": rhp.GEN_CHUNKED, "fuzz": rhp.GEN_FUZZ_HTTP}[case]
@@ -332,4 +332,5 @@ def test_gpu_pack_dense_equals_cpu_pack(case):
     nh = np.where((want_d.reshape(n, 8)[:, 7] & rhp.DENSE_WIDE) == 0, want_d.reshape(n, 8)[:, 5], 0)
     used = np.arange(maxh)[:, None] < nh[None, :]
     assert (got_l.reshape(maxh, n)[used] == want_l.reshape(maxh, n)[used]).all()
-    assert check_pack(res, n, maxh) > 0
+    dense = check_pack(res, n, maxh)
+    assert dense > 0 if case != "chunked" else dense == 0   # (de-framed chunked bodies: all wide)

@@ -1,6 +1,6 @@
 """A large GPU fuzz run against the oracle (a one-off check beside the GPU suite's
 60K-request fuzz): N fuzz requests (GEN_FUZZ phr, GEN_FUZZ_HTTP http) per seed,
-every record layout, the kernel's records against the oracle's and its
+every record layout (round 6: the dense ones too), the kernel's records against the oracle's and its
 DFA / exact-path choice (flags) against the emulator's.  Prints one line per
 case; exits 1 on the first mismatch.
 
@@ -26,7 +26,10 @@ def main():
             buf, off = rhp.generate(gen, n, 7100 + seed)
             for maxh in (0, 3, 16, 64):
                 want = to_rhp(*run_oracle(buf, off, maxh, mode)[:3], mode)
-                for layout in (rhp.LAYOUT_REQUEST_MAJOR, rhp.LAYOUT_HEADER_MAJOR, rhp.LAYOUT_COMPACT):
+                lays = [rhp.LAYOUT_REQUEST_MAJOR, rhp.LAYOUT_HEADER_MAJOR, rhp.LAYOUT_COMPACT, rhp.LAYOUT_DENSE]
+                if mode == rhp.MODE_PHR:
+                    lays.append(rhp.LAYOUT_DENSE_RM)   # (request-major dense: phr mode only)
+                for layout in lays:
                     res = rhp.parse_batch(buf, off, maxh, mode, layout=layout)
                     assert_same(canon(res, mode), want, buf, off, f"fuzz seed {seed} mode {mode} maxh {maxh} layout {layout}")
                     emu, _ = rhp.emulate(buf, off, maxh, mode, layout)

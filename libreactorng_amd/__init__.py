@@ -487,11 +487,15 @@ class DeviceBatch:
                      self.http.data_ptr(), self.work.data_ptr(), self.flags, 0,
                      self.last_len.data_ptr() if self.last_len is not None else None)
 
+    _runtime_checked = False   # one /proc/self/maps scan per process (it costs ~0.2 ms: not per launch)
+
     def launch(self, stream=None) -> None:
         import torch
         s = stream if stream is not None else torch.cuda.current_stream()
         d = self.desc()
-        check_one_hip_runtime()
+        if not DeviceBatch._runtime_checked:
+            check_one_hip_runtime()   # the device buffers were allocated by torch's runtime by now
+            DeviceBatch._runtime_checked = True
         rc = lib().rhp_parse_batch(ctypes.byref(d), ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
             raise RuntimeError(f"rhp_parse_batch failed: {rc}")

@@ -1781,6 +1781,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
    * fourth step: config 2 +3 %). */
   auto walk = [&]() {
     uint32_t c[8], r[8];
+#if defined(RHP_DIAG_EXTRA_LDS) || defined(RHP_DIAG_EXTRA_VALU)
+    uint32_t xacc = 0;   /* diagnostic: one more LDS read / three more VALU per pair (the walk's sensitivity) */
+#endif
     codes_a(W[0], r);
     codes_b(W[0], r, c);
 #pragma unroll
@@ -1793,6 +1796,18 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         __builtin_amdgcn_sched_barrier(0);   /* the chained read issues first */
         if (nx) r[j] = look_a(W[q + 1][j >> 1], j);
         if (nx && j > 0) cn[j - 1] = look_b(r[j - 1], W[q + 1][(j - 1) >> 1], j - 1);
+#ifdef RHP_DIAG_EXTRA_LDS
+        if (nx) xacc += lds_u8(__builtin_amdgcn_perm(kClassRow, W[q + 1][j >> 1], 0x0c0c0400u | (uint32_t) (2 * (j & 1))));
+#endif
+#ifdef RHP_DIAG_EXTRA_VALU
+        if (nx) {
+          uint32_t y = __builtin_amdgcn_perm(W[q + 1][j >> 1], W[q + 1][j >> 1], 0x0c0c0001u + 0x202u * (uint32_t) (j & 1));
+          opaque(y);
+          y = y ^ ((y >> 6) & 0x7cu);
+          opaque(y);
+          xacc += y;
+        }
+#endif
         __builtin_amdgcn_sched_barrier(0);
         ev_shift2(ev[q >> 1], st);
         __builtin_amdgcn_sched_barrier(0);
@@ -1809,6 +1824,9 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
       if constexpr (kPhaseLock)
         if ((q & 1) && nx && !__builtin_amdgcn_ballot_w64(st >= kLiveIdx)) break;
     }
+#if defined(RHP_DIAG_EXTRA_LDS) || defined(RHP_DIAG_EXTRA_VALU)
+    asm volatile("" ::"v"(xacc));
+#endif
   };
 
   /* The bytes of a first window before its request (wlead of them) zeroed in
@@ -2576,6 +2594,11 @@ int launch_dfa(const Params &prm, hipStream_t s, int dev, int cus)
   return (int) hipGetLastError();
 }
 
+/* waves per workgroup of the phr-mode kernels (16: four per SIMD) */
+#ifndef RHP_PHR_WAVES
+#define RHP_PHR_WAVES 16
+#endif
+
 /* the late-issue form: http mode (frames requests in the loop), or on request
  * (RHP_IMPL_DFA_LATE, parity tests of that form in phr mode) */
 bool late_issue(uint32_t mode) { return t_impl == RHP_IMPL_DFA_LATE || mode == RHP_MODE_HTTP; }
@@ -2704,10 +2727,11 @@ int rhp_parse_batch(const rhp_batch_t *b, void *stream)
     return dense     ? launch_dfa<kHttpWaves, true, true, kRecDense>(prm, s, dev, cus)
            : compact ? launch_dfa<kHttpWaves, true, true, kRecCompact>(prm, s, dev, cus)
                      : launch_dfa<kHttpWaves, true, true, kRecWide>(prm, s, dev, cus);
-  if (dense) return late ? launch_dfa<16, true, false, kRecDense>(prm, s, dev, cus) : launch_dfa<16, false, false, kRecDense>(prm, s, dev, cus);
-  if (compact) return late ? launch_dfa<16, true, false, kRecCompact>(prm, s, dev, cus) : launch_dfa<16, false, false, kRecCompact>(prm, s, dev, cus);
-  if (late) return launch_dfa<16, true, false, kRecWide>(prm, s, dev, cus);
-  return launch_dfa<16, false, false, kRecWide>(prm, s, dev, cus);
+  constexpr int W = RHP_PHR_WAVES;
+  if (dense) return late ? launch_dfa<W, true, false, kRecDense>(prm, s, dev, cus) : launch_dfa<W, false, false, kRecDense>(prm, s, dev, cus);
+  if (compact) return late ? launch_dfa<W, true, false, kRecCompact>(prm, s, dev, cus) : launch_dfa<W, false, false, kRecCompact>(prm, s, dev, cus);
+  if (late) return launch_dfa<W, true, false, kRecWide>(prm, s, dev, cus);
+  return launch_dfa<W, false, false, kRecWide>(prm, s, dev, cus);
 }
 
 int rhp_pack_dense(const rhp_batch_t *b, rhp_req_dense_t *dreq, rhp_http_compact_t *hc, uint16_t *lens16, void *stream)

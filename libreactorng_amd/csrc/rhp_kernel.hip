@@ -743,8 +743,11 @@ __device__ __forceinline__ bool frame_chunked(uint8_t *b, uint64_t len, int32_t 
  * Every global load of a group lands before its stores (each chunk's data lies
  * at or past its destination, and bodies do not overlap).  Slot reads stay
  * below lead + region + 20 <= kStageBody (frame_chunked's staging test). */
+/* bytes of a wave's chunk tables (staged_moves: one per body slot) */
+constexpr uint32_t kChunkTab = 8u * (kMoveChunks + 1u), kChunkTabWave = kChunkTab * kStageBodies;
 template <class Step>
-__device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, uint32_t lane, uint32_t stage, Step &&step)
+__device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, uint32_t lane, uint32_t stage, uint32_t ctab,
+                                             Step &&step)
 {
   typedef __attribute__((address_space(1))) const u32x4 gq;
   typedef __attribute__((address_space(1))) u32x4 gw;
@@ -796,17 +799,21 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
                  __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r)};
   };
   /* out's bytes k >= s (0 < s < 16) from o */
-  auto merge_from = [](u32x4 &out, const u32x4 &o, int32_t s) {
+  /* the bytes k >= s (0 <= s <= 16) of a 16-byte block as a mask: two 64-bit
+   * shifts and their selects, not a clamp and shift per dword */
+  auto from_mask = [](int32_t s) -> u32x4 {
+    const uint32_t a = 8u * (uint32_t) min(max(s, 0), 16);   /* bits below the first byte taken */
+    const uint64_t lo = a >= 64u ? 0ull : ~0ull << a;
+    const uint64_t hi = a <= 64u ? ~0ull : a >= 128u ? 0ull : ~0ull << (a - 64u);
+    return u32x4{(uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32)};
+  };
+  auto merge_from = [&](u32x4 &out, const u32x4 &o, int32_t s) {
+    const u32x4 msk = from_mask(s);
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int32_t c = min(max(s - 4 * j, 0), 4);
-      const uint32_t msk = c >= 4 ? 0u : ~0u << (8 * c);
-      out[j] = (o[j] & msk) | (out[j] & ~msk);
-    }
+    for (int j = 0; j < 4; j++) out[j] = (o[j] & msk[j]) | (out[j] & ~msk[j]);
   };
   auto build = [&](uint32_t q, uint32_t owner) {
     const uint64_t base = base_of(owner);
-    const uint32_t nch = __builtin_amdgcn_readlane(sb.nch, owner);
     int32_t cd[kMoveChunks + 1], dl[kMoveChunks];   /* body offset of chunk c; its slot shift src - dst (scalar) */
     cd[0] = 0;
 #pragma unroll
@@ -821,33 +828,45 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
     const uint64_t a0 = base - lead;
     const uint32_t blocks = (lead + (uint32_t) L + 15u) >> 4;
     const uint32_t slot = stage + kStageBody * q;
+    /* The body's chunk table in LDS, T[c] = {dl[c], cd[c + 1]} (T[kMoveChunks] =
+     * {0, L}), written by one lane: a lane reads its block's chunk c and the
+     * next one as T[c], T[c + 1] in one ds_read2_b64 instead of selecting them
+     * from the scalars (a select chain with a v_mov per scalar operand: ~70
+     * instructions per block, chunked config) */
+    typedef __attribute__((address_space(3))) u32x2 lq2;
+    const uint32_t tab = ctab + kChunkTab * q;
+    if (lane == 0) {
+#pragma unroll
+      for (uint32_t c = 0; c <= kMoveChunks; c++)
+        *reinterpret_cast<lq2 *>((size_t) (tab + 8u * c)) =
+            u32x2{c < kMoveChunks ? (uint32_t) dl[c] : 0u, (uint32_t) (c < kMoveChunks ? cd[c + 1] : L)};
+    }
+    __builtin_amdgcn_wave_barrier();   /* the wave's LDS accesses stay in order: every lane reads T after lane 0 wrote it */
     for (uint32_t b = lane; b < blocks; b += 64u) {
-      /* block b: body offsets [t0, t0 + 16); chunk c holds its first byte */
+      /* block b: body offsets [t0, t0 + 16); chunk c holds its first byte (the
+       * chunks past nch start at L > t0: they never count) */
       const int32_t t0 = (int32_t) (16u * b) - (int32_t) lead;
       uint32_t c = 0;
-      int32_t d0 = dl[0], d1 = dl[1], e0 = cd[1], e1 = cd[2];
 #pragma unroll
-      for (uint32_t j = 1; j < kMoveChunks; j++) {
-        if (j < nch && cd[j] <= t0) {
-          c = j;
-          d0 = dl[j];
-          e0 = cd[j + 1];
-          d1 = j + 1 < kMoveChunks ? dl[j + 1] : 0;
-          e1 = j + 1 < kMoveChunks ? cd[j + 2] : L;
-        }
-      }
-      u32x4 out = fetch(slot, 16u * b + (uint32_t) d0);
-      bool more = false;
-      if (c + 1 < nch && e0 < t0 + 16) {   /* the next chunk starts inside the block */
-        merge_from(out, fetch(slot, 16u * b + (uint32_t) d1), e0 - t0);
-        more = c + 2 < nch && e1 < t0 + 16;
-      }
-      if (__builtin_amdgcn_ballot_w64(more)) {   /* a chunk of < 16 bytes: every later chunk starting in the block */
-#pragma unroll
-        for (uint32_t j = 2; j < kMoveChunks; j++) {
-          const bool take_j = j < nch && more && j >= c + 2 && cd[j] < t0 + 16;
-          if (__builtin_amdgcn_ballot_w64(take_j) && take_j)
-            merge_from(out, fetch(slot, 16u * b + (uint32_t) dl[j]), cd[j] - t0);
+      for (uint32_t j = 1; j < kMoveChunks; j++) c += cd[j] <= t0 ? 1u : 0u;
+      const u32x2 T0 = *reinterpret_cast<const lq2 *>((size_t) (tab + 8u * c));
+      u32x2 Tn = *reinterpret_cast<const lq2 *>((size_t) (tab + 8u * c + 8u));
+      u32x4 out = fetch(slot, 16u * b + T0[0]);
+      /* the chunks that start inside the block, in order (usually none or one;
+       * a chunk of < 16 bytes brings the next): chunk j's bytes from its start
+       * e on (T[j - 1].y = cd[j]; j < nch while e < L) */
+      int32_t ej = (int32_t) T0[1];
+      uint32_t tj = tab + 8u * c + 16u;
+      bool more = ej < L && ej < t0 + 16;
+      while (__builtin_amdgcn_ballot_w64(more)) {
+        if (more) {
+          merge_from(out, fetch(slot, 16u * b + Tn[0]), ej - t0);
+          ej = (int32_t) Tn[1];
+          more = ej < L && ej < t0 + 16;
+          if (more) {
+            Tn = *reinterpret_cast<const lq2 *>((size_t) tj);
+            tj += 8u;
+          }
         }
       }
       const uintptr_t A = (uintptr_t) (a0 + 16u * b);
@@ -861,11 +880,11 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
       const bool whole = inner || t0 + 16 <= size;
       if (!inner && whole) {
         const u32x4 orig = *reinterpret_cast<const lq *>((size_t) (slot + 16u * b));
-        const int32_t kb = max(-t0, 0), ke = min(L - t0, 16);
+        /* the body's bytes [kb, ke) of the block from out, the rest as in memory */
+        const u32x4 mb = from_mask(-t0), me = from_mask(L - t0);
 #pragma unroll
         for (int32_t j = 0; j < 4; j++) {
-          const int32_t lo = min(max(kb - 4 * j, 0), 4), hi = min(max(ke - 4 * j, 0), 4);
-          const uint32_t msk = hi > lo ? (~0u >> (32 - 8 * (hi - lo))) << (8 * lo) : 0u;
+          const uint32_t msk = mb[j] & ~me[j];
           out[j] = (out[j] & msk) | (orig[j] & ~msk);
         }
       }
@@ -2332,7 +2351,7 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
      * holds the chunked bodies' LDS slots (staged_moves) */
     uint32_t *slow = reinterpret_cast<uint32_t *>(lds);
     uint32_t *slow_n = wg_counter + 4;                                 /* 0 since the prologue */
-    constexpr uint32_t kSlowCap = kLdsTable / 4;
+    constexpr uint32_t kSlowCap = (kLdsTable - (uint32_t) WAVES * kChunkTabWave) / 4;   /* the chunk tables at the area's end */
     static_assert(kStageBody * kStageBodies <= kStageWave, "a wave's body slots fit its staging");
     dg.pass_begin();
     /* the deferred requests: the list finalize kept, or the whole range when
@@ -2453,7 +2472,8 @@ __global__ __launch_bounds__(WAVES * 64, RHP_WAVES_PER_SIMD) void rhp_dfa_kernel
         if (kn.x < ns) start_round(kn.x, kn.y);
         else walking = w.live = false;
         dg.part_begin();
-        if (m) staged_moves(m, sb, lane, stage, [&]() { w.step(); });
+        if (m) staged_moves(m, sb, lane, stage, kLdsTable - (uint32_t) WAVES * kChunkTabWave + (tid >> 6) * kChunkTabWave,
+                            [&]() { w.step(); });
         dg.part_end(5);
       } else {
         if (kn.x < ns) start_round(kn.x, kn.y);

@@ -281,12 +281,22 @@ int main()
     return 0;
   }
   if (getenv("LINES2")) {   /* depth, wave count and record bytes of the alt order */
-#define RUN2(NW, DEPTH, REC, TWO, NAME)                                                                            \
+#define RUN2G(NW, DEPTH, REC, TWO, G, EXTRA, NAME)                                                                  \
   do {                                                                                                             \
-    const size_t l2 = (size_t) NW * DEPTH * 8192;                                                                  \
+    const size_t l2 = (size_t) NW * DEPTH * 8192 + (EXTRA);                                                        \
     CHECK(hipFuncSetAttribute((const void *) lines2<NW, DEPTH, REC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) l2)); \
-    run(NAME, [&](uint8_t *b, hipStream_t s) { hipLaunchKernelGGL((lines2<NW, DEPTH, REC>), dim3(cus), dim3(NW * 64), l2, s, b, lens, out); }, in, kBytes, TWO); \
+    run(NAME, [&](uint8_t *b, hipStream_t s) { hipLaunchKernelGGL((lines2<NW, DEPTH, REC>), dim3(cus * (G)), dim3(NW * 64), l2, s, b, lens, out); }, in, kBytes, TWO); \
   } while (0)
+#define RUN2(NW, DEPTH, REC, TWO, NAME) RUN2G(NW, DEPTH, REC, TWO, 1, 0, NAME)
+    if (getenv("LINES2_WG")) {   /* one 16-wave workgroup per CU against two 8-wave ones (80 KB of LDS each) */
+      for (int rep = 0; rep < 3; rep++) {
+        RUN2G(16, 1, 2, false, 1, 27 * 1024, "1 x 16 waves per CU, 16 B dense, one stream");
+        RUN2G(16, 1, 2, true, 1, 27 * 1024, "1 x 16 waves per CU, 16 B dense, two streams");
+        RUN2G(8, 1, 2, false, 2, 15 * 1024, "2 x 8 waves per CU, 16 B dense, one stream");
+        RUN2G(8, 1, 2, true, 2, 15 * 1024, "2 x 8 waves per CU, 16 B dense, two streams");
+      }
+      return 0;
+    }
     for (int rep = 0; rep < 2; rep++) {
       RUN2(16, 1, 3, false, "16 waves x 1 deep, 16 B one dwordx4 wt");
       RUN2(16, 1, 5, false, "16 waves x 1 deep, 16 B one dwordx4 plain");

@@ -669,7 +669,8 @@ struct StagedBody {
   uint64_t base;           /* the body's first byte: the de-framed body goes to [base, base + len) */
   uint32_t nch, region;    /* data chunks; framed bytes up to the last data byte */
   uint32_t size;           /* the body's bytes up to the request's end (capped at 2 * kStageBody) */
-  uint32_t span[kMoveChunks];   /* chunk c's data: [base + (span & 0xffff), + (span >> 16)) (< kStageBody) */
+  uint32_t span[kMoveChunks];   /* chunk c: its slot shift src - dst | the body offset where chunk c + 1 starts << 16
+                                   (a chunk past the body's: 0 | L << 16; both < kStageBody) */
 };
 __device__ __forceinline__ bool finish_chunked(const ChunkWalk &w, int32_t ret, rhp_http_t *x, bool compact,
                                                StagedBody *sb)
@@ -689,8 +690,14 @@ __device__ __forceinline__ bool finish_chunked(const ChunkWalk &w, int32_t ret, 
     sb->nch = w.k;
     sb->region = (uint32_t) w.region;
     sb->size = (uint32_t) min(w.size, (uint64_t) (2 * kStageBody));
+    uint32_t cdv = 0;   /* the chunk table entries of staged_moves: dl | cd_next << 16 (see StagedBody) */
 #pragma unroll
-    for (uint32_t j = 0; j < kMoveChunks; j++) sb->span[j] = j < w.k ? w.span[j] : 0u;
+    for (uint32_t j = 0; j < kMoveChunks; j++) {
+      const uint32_t sp = j < w.k ? w.span[j] : 0u;
+      const uint32_t dl = j < w.k ? (sp & 0xffffu) - cdv : 0u;
+      cdv += sp >> 16;
+      sb->span[j] = dl | cdv << 16;
+    }
     return true;
   }
   DevMove M{w.in};
@@ -744,7 +751,7 @@ __device__ __forceinline__ bool frame_chunked(uint8_t *b, uint64_t len, int32_t 
  * at or past its destination, and bodies do not overlap).  Slot reads stay
  * below lead + region + 20 <= kStageBody (frame_chunked's staging test). */
 /* bytes of a wave's chunk tables (staged_moves: one per body slot) */
-constexpr uint32_t kChunkTab = 8u * (kMoveChunks + 1u), kChunkTabWave = kChunkTab * kStageBodies;
+constexpr uint32_t kChunkTab = 4u * (kMoveChunks + 1u), kChunkTabWave = kChunkTab * kStageBodies;
 template <class Step>
 __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, uint32_t lane, uint32_t stage, uint32_t ctab,
                                              Step &&step)
@@ -814,32 +821,32 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
   };
   auto build = [&](uint32_t q, uint32_t owner) {
     const uint64_t base = base_of(owner);
-    int32_t cd[kMoveChunks + 1], dl[kMoveChunks];   /* body offset of chunk c; its slot shift src - dst (scalar) */
-    cd[0] = 0;
+    /* the body's chunk table T[c] = dl[c] | cd[c + 1] << 16 (dl: chunk c's slot
+     * shift src - dst, cd: body offsets of the chunk starts; finish_chunked
+     * packed them), T[kMoveChunks] = L << 16 */
+    uint32_t T[kMoveChunks];
+    int32_t cd[kMoveChunks];   /* cd[j] = T[j - 1] >> 16, j = 1 .. kMoveChunks - 1: the block's chunk count */
 #pragma unroll
-    for (uint32_t c = 0; c < kMoveChunks; c++) {
-      const uint32_t sp = __builtin_amdgcn_readlane(sb.span[c], owner);
-      dl[c] = (int32_t) (sp & 0xffffu) - cd[c];
-      cd[c + 1] = cd[c] + (int32_t) (sp >> 16);
-    }
-    const int32_t L = cd[kMoveChunks];   /* spans past nch are empty */
+    for (uint32_t c = 0; c < kMoveChunks; c++) T[c] = __builtin_amdgcn_readlane(sb.span[c], owner);
+#pragma unroll
+    for (uint32_t j = 1; j < kMoveChunks; j++) cd[j] = (int32_t) (T[j - 1] >> 16);
+    const int32_t L = (int32_t) (T[kMoveChunks - 1] >> 16);   /* spans past the body's chunks are empty */
     const int32_t size = (int32_t) __builtin_amdgcn_readlane(sb.size, owner);
     const uint32_t lead = (uint32_t) base & 15u;
     const uint64_t a0 = base - lead;
     const uint32_t blocks = (lead + (uint32_t) L + 15u) >> 4;
     const uint32_t slot = stage + kStageBody * q;
-    /* The body's chunk table in LDS, T[c] = {dl[c], cd[c + 1]} (T[kMoveChunks] =
-     * {0, L}), written by one lane: a lane reads its block's chunk c and the
-     * next one as T[c], T[c + 1] in one ds_read2_b64 instead of selecting them
-     * from the scalars (a select chain with a v_mov per scalar operand: ~70
-     * instructions per block, chunked config) */
-    typedef __attribute__((address_space(3))) u32x2 lq2;
+    /* The table in LDS, written by one lane: a lane reads its block's chunk c
+     * and the next one as T[c], T[c + 1] with one ds_read2_b32 instead of
+     * selecting them from the scalars (a select chain with a v_mov per scalar
+     * operand: ~70 instructions per block, chunked config) */
+    typedef __attribute__((address_space(3))) uint32_t lq1;
+    typedef __attribute__((address_space(3))) u32x4 lq4;
     const uint32_t tab = ctab + kChunkTab * q;
     if (lane == 0) {
-#pragma unroll
-      for (uint32_t c = 0; c <= kMoveChunks; c++)
-        *reinterpret_cast<lq2 *>((size_t) (tab + 8u * c)) =
-            u32x2{c < kMoveChunks ? (uint32_t) dl[c] : 0u, (uint32_t) (c < kMoveChunks ? cd[c + 1] : L)};
+      *reinterpret_cast<lq4 *>((size_t) tab) = u32x4{T[0], T[1], T[2], T[3]};
+      *reinterpret_cast<lq4 *>((size_t) (tab + 16u)) = u32x4{T[4], T[5], T[6], T[7]};
+      *reinterpret_cast<lq1 *>((size_t) (tab + 32u)) = (uint32_t) L << 16;
     }
     __builtin_amdgcn_wave_barrier();   /* the wave's LDS accesses stay in order: every lane reads T after lane 0 wrote it */
     for (uint32_t b = lane; b < blocks; b += 64u) {
@@ -849,23 +856,23 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
       uint32_t c = 0;
 #pragma unroll
       for (uint32_t j = 1; j < kMoveChunks; j++) c += cd[j] <= t0 ? 1u : 0u;
-      const u32x2 T0 = *reinterpret_cast<const lq2 *>((size_t) (tab + 8u * c));
-      u32x2 Tn = *reinterpret_cast<const lq2 *>((size_t) (tab + 8u * c + 8u));
-      u32x4 out = fetch(slot, 16u * b + T0[0]);
+      const uint32_t T0 = *reinterpret_cast<const lq1 *>((size_t) (tab + 4u * c));
+      uint32_t Tn = *reinterpret_cast<const lq1 *>((size_t) (tab + 4u * c + 4u));
+      u32x4 out = fetch(slot, 16u * b + (T0 & 0xffffu));
       /* the chunks that start inside the block, in order (usually none or one;
        * a chunk of < 16 bytes brings the next): chunk j's bytes from its start
-       * e on (T[j - 1].y = cd[j]; j < nch while e < L) */
-      int32_t ej = (int32_t) T0[1];
-      uint32_t tj = tab + 8u * c + 16u;
+       * e on (T[j - 1] >> 16 = cd[j]; a real chunk while e < L) */
+      int32_t ej = (int32_t) (T0 >> 16);
+      uint32_t tj = tab + 4u * c + 8u;
       bool more = ej < L && ej < t0 + 16;
       while (__builtin_amdgcn_ballot_w64(more)) {
         if (more) {
-          merge_from(out, fetch(slot, 16u * b + Tn[0]), ej - t0);
-          ej = (int32_t) Tn[1];
+          merge_from(out, fetch(slot, 16u * b + (Tn & 0xffffu)), ej - t0);
+          ej = (int32_t) (Tn >> 16);
           more = ej < L && ej < t0 + 16;
           if (more) {
-            Tn = *reinterpret_cast<const lq2 *>((size_t) tj);
-            tj += 8u;
+            Tn = *reinterpret_cast<const lq1 *>((size_t) tj);
+            tj += 4u;
           }
         }
       }

@@ -766,6 +766,7 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
   struct Group {
     uint32_t owner[kStageBodies];   /* the lane whose body slot q holds (a valid lane for an empty slot) */
     uint32_t have;                  /* bit q: slot q holds a body */
+    uint32_t wide;                  /* bit q: slot q's body has lines past the first 64 (their loads were made) */
   };
   auto take = [&](Group &g) {
     g.have = 0;
@@ -784,7 +785,8 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
   typedef u32x4 Lines[kStageBodies][kLinesPerLane];
   /* a group's framed lines (lines past a body's region load its first line;
    * an empty slot loads its group's first body's first line) */
-  auto load = [&](const Group &g, Lines &raw) {
+  auto load = [&](Group &g, Lines &raw) {
+    g.wide = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kStageBodies; q++) {
       const uint64_t base = base_of(g.owner[q]);
@@ -794,7 +796,10 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
 #pragma unroll
       for (uint32_t h = 0; h < kLinesPerLane; h++) {
         const uint32_t line = lane + 64u * h;
-        raw[q][h] = *reinterpret_cast<gq *>((uintptr_t) (la + (line < lines ? 16u * line : 0u)));
+        if (h == 0 || 64u * h < lines) {   /* wave-uniform: a body of at most 64 lines loads one line per lane */
+          raw[q][h] = *reinterpret_cast<gq *>((uintptr_t) (la + (line < lines ? 16u * line : 0u)));
+          if (h) g.wide |= 1u << q;
+        }
       }
     }
   };
@@ -912,12 +917,13 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
       }
     }
   };
-  auto to_slots = [&](const Lines &raw) {
+  auto to_slots = [&](const Group &g, const Lines &raw) {
 #pragma unroll
     for (uint32_t q = 0; q < kStageBodies; q++)
 #pragma unroll
       for (uint32_t h = 0; h < kLinesPerLane; h++)
-        *reinterpret_cast<lq *>((size_t) (stage + kStageBody * q + 16u * (lane + 64u * h))) = raw[q][h];
+        if (h == 0 || (g.wide >> q & 1u))   /* lines past a body's region were not loaded: their slot bytes are not read */
+          *reinterpret_cast<lq *>((size_t) (stage + kStageBody * q + 16u * (lane + 64u * h))) = raw[q][h];
     wait_lgkm0();   /* the wave's slots are written (a wave reads its own) */
   };
   auto build_group = [&](const Group &g) {
@@ -930,7 +936,7 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
   take(g);
   load(g, ra);
   while (g.have) {
-    to_slots(ra);
+    to_slots(g, ra);
     step();   /* the caller's per-group work (the next round's walks): its loads go out before the next group's */
     Group gn;
     take(gn);

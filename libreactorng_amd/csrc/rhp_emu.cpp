@@ -341,6 +341,18 @@ extern "C" int rhp_test_chunk_window(const uint8_t *line, uint32_t nw, uint64_t 
   return one_chunk_window(W, nw, avail, res, doff, dlen) ? 1 : 0;
 }
 
+/* test hook: one_chunk_head over the first 4 * nd bytes at `line` (nd 5: the
+ * GPU replay's 20-byte window, or 8); returns 0 when it leaves the line to
+ * one_chunk_window */
+extern "C" int rhp_test_chunk_head(const uint8_t *line, uint32_t nw, uint64_t avail, int64_t *res, uint64_t *doff,
+                                   uint64_t *dlen, uint32_t nd)
+{
+  uint32_t W[8];
+  memcpy(W, line, 32);
+  return (nd == 5 ? one_chunk_head<5>(W, nw, avail, res, doff, dlen) : one_chunk_head<8>(W, nw, avail, res, doff, dlen))
+             ? 1 : 0;
+}
+
 /* test hook: the pair table the kernel copies into LDS (rhp_dfa.h make_table2)
  * and its geometry: meta = {bytes, row stride, kClassRowR, kClassRow, idx2(S_SLOW, 1), kClassRow16} */
 extern "C" uint32_t rhp_test_table2(uint8_t *out, uint32_t *meta)

@@ -629,7 +629,10 @@ struct ChunkWalk {
     int64_t r;
     uint64_t doff = 0, dlen = 0;
     /* W holds 20 bytes from the line's start, of them 32 - (a & 15) >= 17 in the two lines */
-    if (!one_chunk_window(W, min(20u, 32u - ((uint32_t) a & 15u)), size - off, &r, &doff, &dlen)) {
+    /* the common line without a byte loop (one_chunk_head), else the windowed
+     * state machine, else the byte-wise parse past the window */
+    const uint32_t nw = min(20u, 32u - ((uint32_t) a & 15u));
+    if (!one_chunk_head<5>(W, nw, size - off, &r, &doff, &dlen) && !one_chunk_window(W, nw, size - off, &r, &doff, &dlen)) {
       LineBytes B{in, ~0ull, {0, 0, 0, 0}};
       r = one_chunk_t(B, off, size, &doff, &dlen);
     }

@@ -395,6 +395,75 @@ RHP_HD bool one_chunk_window(const uint32_t (&W)[8], uint32_t nw, uint64_t avail
   return true;
 }
 
+/* one_chunk_window's answer for the common size line, without its byte loop's
+ * branches (round 6, the GPU replay's size-line walk): the LF found by a
+ * zero-byte test on the window's first ND dwords (nw <= 4 * ND), the state
+ * machine run over the first 8 bytes only, every byte under a predicate.  A
+ * line whose state is decided by its 8th byte -- an extension or its CR
+ * reached, or an error --, or whose LF comes earlier, is answered here with
+ * one_chunk_window's result; anything else (a longer run of OWS or hex digits)
+ * returns false and the caller runs one_chunk_window.  At most 8 digits are
+ * read, so the size fits 32 bits and never overflows. */
+template <uint32_t ND>
+RHP_HD bool one_chunk_head(const uint32_t (&W)[8], uint32_t nw, uint64_t avail, int64_t *res, uint64_t *data_off,
+                           uint64_t *data_len)
+{
+  enum : uint32_t { kLead, kHex, kTrail, kExt, kCr, kErr };
+  uint32_t nl = 32;   /* the first LF among the window's bytes, 32: none */
+#pragma unroll
+  for (int q = (int) ND - 1; q >= 0; q--) {   /* the lowest dword with an LF wins; the first zero byte is exact */
+    const uint32_t t = W[q] ^ 0x0a0a0a0au;
+    const uint32_t z = (t - 0x01010101u) & ~t & 0x80808080u;
+    nl = z ? 4u * (uint32_t) q + ((uint32_t) __builtin_ctz(z) >> 3) : nl;
+  }
+  nl = nl < nw ? nl : 32u;
+  if (nl == 32 && avail > nw) return false;
+  if (nl >= avail) {   /* no LF within the body yet */
+    *res = 0;
+    return true;
+  }
+  uint32_t st = kLead, cs = 0;
+  bool prev_cr = false;
+#pragma unroll
+  for (uint32_t j = 0; j < 8; j++) {
+    const uint32_t c = (W[j >> 2] >> (8 * (j & 3))) & 0xffu;
+    const bool live = j < nl;
+    const bool ows = is_ows(c);
+    const uint32_t dg = c - '0', al = (c | 0x20u) - 'a';
+    const bool hex = dg < 10u || al < 6u;
+    const bool dig = st <= kHex && hex;
+    const uint32_t nst = dig ? kHex
+                         : st == kLead ? (ows ? kLead : kErr)
+                         : (st == kHex || st == kTrail) ? (ows ? kTrail : c == ';' ? kExt : c == '\r' ? kCr : kErr)
+                         : st == kCr ? kErr : st;
+    cs = live && dig ? (cs << 4) | (dg < 10u ? dg : al + 10u) : cs;
+    st = live ? nst : st;
+    prev_cr = live ? c == '\r' : prev_cr;
+  }
+  if (nl > 8) {   /* bytes 8 .. nl - 1 not run */
+    if (st <= kTrail) return false;   /* OWS / digits / OWS still running: one_chunk_window decides */
+    if (st == kCr) st = kErr;          /* byte 8 follows the CR: not its LF */
+    const uint32_t b = nl - 1;         /* an extension: what counts is the byte before the LF */
+    uint32_t wd = W[0];
+#pragma unroll
+    for (uint32_t q = 1; q < ND; q++) wd = (b >> 2) == q ? W[q] : wd;
+    prev_cr = ((wd >> (8 * (b & 3))) & 0xffu) == '\r';
+  }
+  if (!(st == kCr || (st == kExt && prev_cr))) {
+    *res = -1;
+    return true;
+  }
+  const uint64_t n = nl + 1;
+  if (n + 2 > avail || cs > avail - n - 2) {
+    *res = 0;
+    return true;
+  }
+  *data_off = n;
+  *data_len = cs;
+  *res = (int64_t) (cs + n + 2);
+  return true;
+}
+
 /* http_dechunk (http.c:134-160): validate every chunk, then move the payloads
  * down in place, chunk by chunk (dst <= src: the compacted body never passes
  * the next size line).  B reads the body (B(p) = body byte p), move(dst, src, n)

@@ -230,6 +230,55 @@ def test_chunk_window_equals_one_chunk_t():
     assert decided > 50000
 
 
+def test_chunk_head_equals_one_chunk_t():
+    """The replay's branch-free size-line parse (rhp_scalar.h one_chunk_head: the
+    LF by a zero-byte test, the state machine over the first 8 bytes) against the
+    byte-wise one_chunk_t (http.c:73-132) and one_chunk_window, on the same kind
+    of random size lines as above, for the kernel's 20-byte window (5 dwords,
+    nw 17-20) and a 32-byte one: wherever it decides, the result and the data
+    span are one_chunk_t's; it decides every well-formed line of this workload's
+    shape (OWS, up to 8 digits or an extension within 8 bytes)."""
+    import ctypes
+    import random
+    h = rhp.host()
+    h.rhp_test_chunk_head.restype = ctypes.c_int
+    h.rhp_test_chunk_head.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64] + [ctypes.c_void_p] * 3 + [ctypes.c_uint32]
+    h.rhp_test_chunk_window.restype = ctypes.c_int
+    h.rhp_test_chunk_window.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64] + [ctypes.c_void_p] * 3
+    h.rhp_test_chunk_exact.restype = ctypes.c_int64
+    alpha = b"0123456789abcdefABCDEF \t;\r\nxgz=\x00" + b"0" * 8 + b"\r\n" * 4
+    rng = random.Random(7)
+    res, doff, dlen = ctypes.c_int64(), ctypes.c_uint64(), ctypes.c_uint64()
+    d2, l2 = ctypes.c_uint64(), ctypes.c_uint64()
+    decided = common = 0
+    for it in range(80000):
+        kind = it % 4
+        short = kind == 0 and it % 8 == 0   # the bench workload's shape
+        if kind == 0:
+            line = (b" " * rng.randrange(2 if short else 3) + f"{rng.randrange(1 << rng.randrange(1, 12 if short else 64)):x}".encode()
+                    + rng.choice([b"", b"\t"] if short else [b"", b"\t", b" \t"])
+                    + rng.choice([b"", b";ext=1", b";a\rb"]) + b"\r\n")
+        else:
+            line = bytes(rng.choice(alpha) for _ in range(rng.randrange(0, 40)))
+        body = line + bytes(rng.randrange(256) for _ in range(rng.randrange(0, 64)))
+        size = rng.randrange(0, len(body) + 1) if rng.random() < 0.5 else len(body)
+        buf = (ctypes.c_uint8 * (size + 128))(*body[:size])
+        want = h.rhp_test_chunk_exact(buf, 0, size, ctypes.byref(d2), ctypes.byref(l2))
+        nd = 5 if it % 2 else 8
+        nw = rng.randrange(17, 21) if nd == 5 else rng.randrange(17, 33)
+        win = (ctypes.c_uint8 * 32)(*(bytes(buf)[:nw] + bytes(rng.randrange(256) for _ in range(32 - nw))))
+        ok = h.rhp_test_chunk_head(win, nw, size, ctypes.byref(res), ctypes.byref(doff), ctypes.byref(dlen), nd)
+        if ok:
+            decided += 1
+            assert res.value == want, (line, size, nw, nd, res.value, want)
+            if want > 0:
+                assert (doff.value, dlen.value) == (d2.value, l2.value), (line, size, nd)
+        if short and size == len(body) and line.find(b";") < 0:
+            common += 1
+            assert ok == 1, (line, size, nw, nd)
+    assert decided > 50000 and common > 1500
+
+
 def test_emulator_chunked_paths_vs_oracle():
     """The GPU's chunked-paths batch (tests/batches.py chunked_paths_batch) through
     the kernel emulation: records and rewritten bytes equal the oracle's."""

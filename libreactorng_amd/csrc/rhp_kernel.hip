@@ -777,7 +777,7 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
     for (uint32_t q = 0; q < kStageBodies; q++) {
       g.owner[q] = m ? (uint32_t) __builtin_ctzll(m) : g.owner[0];
       if (m) g.have |= 1u << q;
-      m &= m ? m - 1 : 0ull;
+      m &= m - 1u;   /* 0 stays 0 */
     }
   };
   auto base_of = [&](uint32_t owner) {
@@ -795,7 +795,7 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
       const uint64_t base = base_of(g.owner[q]);
       const uint32_t region = (g.have >> q & 1u) ? __builtin_amdgcn_readlane(sb.region, g.owner[q]) : 0u;
       const uint64_t la = base & ~(uint64_t) 15;
-      const uint32_t lines = (uint32_t) ((base + region + 15u - la) >> 4);
+      const uint32_t lines = (((uint32_t) base & 15u) + region + 15u) >> 4;   /* 32-bit: region < kStageBody */
 #pragma unroll
       for (uint32_t h = 0; h < kLinesPerLane; h++) {
         const uint32_t line = lane + 64u * h;
@@ -833,11 +833,8 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
      * shift src - dst, cd: body offsets of the chunk starts; finish_chunked
      * packed them), T[kMoveChunks] = L << 16 */
     uint32_t T[kMoveChunks];
-    int32_t cd[kMoveChunks];   /* cd[j] = T[j - 1] >> 16, j = 1 .. kMoveChunks - 1: the block's chunk count */
 #pragma unroll
     for (uint32_t c = 0; c < kMoveChunks; c++) T[c] = __builtin_amdgcn_readlane(sb.span[c], owner);
-#pragma unroll
-    for (uint32_t j = 1; j < kMoveChunks; j++) cd[j] = (int32_t) (T[j - 1] >> 16);
     const int32_t L = (int32_t) (T[kMoveChunks - 1] >> 16);   /* spans past the body's chunks are empty */
     const int32_t size = (int32_t) __builtin_amdgcn_readlane(sb.size, owner);
     const uint32_t lead = (uint32_t) base & 15u;
@@ -862,8 +859,12 @@ __device__ __forceinline__ void staged_moves(uint64_t m, const StagedBody &sb, u
        * chunks past nch start at L > t0: they never count) */
       const int32_t t0 = (int32_t) (16u * b) - (int32_t) lead;
       uint32_t c = 0;
+      /* chunk j >= 1 starts at or below t0 (cd[j] = T[j - 1] >> 16 <= t0): compared on
+       * the packed entry against t0 << 16 | 0xffff, so the boundaries need no unpacking;
+       * a chunk start is >= 1 (entries >= 1 << 16), so t0 < 0 compares against 0 */
+      const uint32_t t0u = t0 < 0 ? 0u : (uint32_t) t0 << 16 | 0xffffu;
 #pragma unroll
-      for (uint32_t j = 1; j < kMoveChunks; j++) c += cd[j] <= t0 ? 1u : 0u;
+      for (uint32_t j = 1; j < kMoveChunks; j++) c += T[j - 1] <= t0u ? 1u : 0u;
       const uint32_t T0 = *reinterpret_cast<const lq1 *>((size_t) (tab + 4u * c));
       uint32_t Tn = *reinterpret_cast<const lq1 *>((size_t) (tab + 4u * c + 4u));
       u32x4 out = fetch(slot, 16u * b + (T0 & 0xffffu));
